@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""bench.py -- GiB/s checksummed, device-resident, one process per GPU.
+
+A step = one RX-verify pass (ip_input.c:459-471 + tcp_input.c:697-720) over one
+batch: for every packet the IPv4 header sum and the TCP pseudo-header sum, both
+computed by one gfx950 kernel launch reading each datagram once
+(mi_cksum_ipv4_verify).  Default workload = BASELINE.json configs[1]: 65536 x
+1500 B IPv4/TCP datagrams in 2176 B rte_mbuf slots (IP header at +142).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1500|9000|64|pareto]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Multi-GPU: packets are independent, so every rank folds its own batch (weak
+scaling, no data-path collective); the process group only carries the barrier
+and the max-over-ranks of the elapsed time.
+
+Rank 0 at N=1 also times the reference CPU path (cpu_baseline: the reference's
+own in_cksum.c from oracle/_ref, or the restatement if that is absent) on a
+bounded sample of the same host bytes, and the host-memory (PCIe-inclusive)
+path.  Prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "GiB/s checksummed (device-resident), batched 1500B & 9000B frames, 1/2/4/8 GPU"
+GIB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+CONFIGS = {
+    # name: (packets per GPU, IP datagram length, slot stride, IP offset in slot)
+    "1500": (65536, 1500, 2176, 142),
+    "9000": (65536, 9000, 9216, 142),
+    "64": (1 << 20, 46, 64, 14),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--config", default="1500", choices=list(CONFIGS) + ["pareto"])
+    ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled (0: enough for >= 1 GiB)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-host-path", action="store_true")
+    return ap.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import libunsod_amd as mi
+    from libunsod_amd import shard, synth
+
+    # ---------------------------------------------------------- workload
+    if args.config == "pareto":
+        total_n = 1 << 22
+        lens_all = synth.pareto_lengths(total_n)
+        lo, hi = shard.shard_by_bytes(lens_all, world, rank)
+        lens = lens_all[lo:hi]
+        n = hi - lo
+        offs = synth.packed_offsets(lens, first_off=2)
+        L_sum = int(lens.sum())
+        size = int(offs[-1] + lens[-1]) + 64 if n else 64
+        workload = f"Pareto 64-9000 B IPv4/TCP RX verify, {total_n} packets split by bytes over {world} GPU(s)"
+        scaling = "strong"
+        cfg = dict(workload=workload, packets_total=total_n, packets_this_rank=n, seed="0x9A7E70", alpha=1.16)
+    else:
+        n, L, stride, first = CONFIGS[args.config]
+        lens = offs = None
+        L_sum = n * L
+        size = first + (n - 1) * stride + L + 64
+        workload = f"{n} x {L} B IPv4/TCP RX verify per GPU (slot stride {stride}, IP at +{first})"
+        scaling = "weak"
+        cfg = dict(workload=workload, packets_per_gpu=n, ip_datagram_len=L, slot_stride=stride, ip_offset=first)
+    size = (size + 255) & ~255
+    R = args.rotate or max(1, -(-(1 << 30) // size))  # footprint >= 1 GiB: defeat the 256 MiB MALL
+    cfg.update(rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
+               parallelism=f"dp{world} (independent packet shards, no collective)")
+
+    batches, outs = [], []
+    for r in range(R):
+        buf = torch.empty(size, dtype=torch.uint8, device=dev)
+        if lens is None:
+            b = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
+        else:
+            b = mi.PktBatch(buf, n, offs=torch.from_numpy(offs.astype(np.int64)).to(dev),
+                            lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()))
+        mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r + 104729 * rank)
+        mi.ipv4_finalize(b)  # TX path makes every packet valid
+        batches.append(b)
+        outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
+                         l4=torch.empty(n, dtype=torch.uint16, device=dev),
+                         status=torch.empty(n, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    # sanity: everything verifies
+    chk = mi.ipv4_verify(batches[0], bad_count=True)
+    torch.cuda.synchronize()
+    if int(chk["bad"].item()) != 0:
+        raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
+
+    stream = torch.cuda.current_stream()
+    for k in range(args.warmup):
+        mi.ipv4_verify(batches[k % R], out=outs[k % R], stream=stream)
+    torch.cuda.synchronize()
+
+    # ------------------------------------------------------- timed region
+    K = args.steps
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev0[k].record(stream)
+        mi.ipv4_verify(batches[k % R], out=outs[k % R], stream=stream)
+        ev1[k].record(stream)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms = [ev0[k].elapsed_time(ev1[k]) for k in range(K)]
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        tot = torch.tensor([float(L_sum)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        job_bytes = float(tot.item()) * K
+        pk = torch.tensor([float(n)], dtype=torch.float64, device=dev)
+        dist.all_reduce(pk)
+        job_pkts = float(pk.item()) * K
+    else:
+        job_bytes = float(L_sum) * K
+        job_pkts = float(n) * K
+    value = job_bytes / elapsed / GIB
+
+    # roofline of the dominant kernel (k_ipv4_verify): algorithmic bytes per
+    # launch = sum(L) read + 5 B written per packet (ip u16, l4 u16, status u8)
+    avg_kern_s = float(np.mean(kern_ms)) / 1e3
+    med_kern_s = float(np.median(kern_ms)) / 1e3
+    alg_bytes = float(L_sum) + 5.0 * n
+    achieved = alg_bytes / avg_kern_s / 1e9
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tfile):
+        try:
+            traffic = json.load(open(tfile)).get(args.config)
+        except Exception:
+            traffic = None
+    roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                kernel="k_ipv4_verify", alg_bytes_per_launch=int(alg_bytes),
+                avg_launch_us=round(avg_kern_s * 1e6, 2), median_launch_us=round(med_kern_s * 1e6, 2))
+
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True,
+        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic: device-generated IPv4/TCP datagrams (splitmix64 payload), TX-finalized to valid sums",
+        "config": cfg, "mpkt_per_s": round(job_pkts / elapsed / 1e6, 2), "roofline": roof,
+    }
+
+    # -------------------------------------------- CPU baseline + host path
+    if world == 1 and rank == 0 and args.config != "pareto":
+        host = batches[0].buf.cpu().numpy()
+        if args.cpu_seconds > 0:
+            result["cpu_baseline"] = cpu_baseline(host, n, L, stride, first, args.cpu_seconds)
+        if not args.no_host_path:
+            result["pcie_inclusive"] = host_path(mi, host, n, L, stride, first)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(host: np.ndarray, n: int, L: int, stride: int, first: int, seconds: float) -> dict:
+    """The reference CPU path on the same bytes: ipv4_verify_batch drives
+    in_cksum_hdr + in_cksum_pseudo_header per packet exactly as ip_input /
+    tcp_input call them.  1 thread, repeated passes over (a prefix of) the batch
+    until `seconds` of CPU work."""
+    from oracle.pyoracle import Oracle, available
+    kind = "reference" if available("reference") else "port"
+    o = Oracle(kind)
+    raw = np.zeros(host.size + 128, np.uint8)
+    s = (-raw.ctypes.data) % 64
+    h = raw[s:s + host.size]
+    h[:] = host
+    ip, l4, st = o.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+    assert not st.any(), "CPU baseline disagrees: batch should verify"
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        o.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+        passes += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return dict(value=round(passes * n * L / dt / GIB, 3), unit="GiB/s", cores=1, kind=kind,
+                sample=f"{passes} passes x {n} x {L} B datagrams ({dt:.1f} s, 1 thread): in_cksum_hdr + "
+                       f"in_cksum_pseudo_header per packet, {'oracle/_ref (reference in_cksum.c)' if kind == 'reference' else 'oracle restatement'}, "
+                       f"gcc -O3 -frename-registers -fno-strict-aliasing",
+                cpu=_cpu_model())
+
+
+def host_path(mi, host: np.ndarray, n: int, L: int, stride: int, first: int, iters: int = 5) -> dict:
+    """PCIe-inclusive rate: the batch starts and ends in (page-locked) host
+    memory; chunked H2D -> verify -> D2H (mi_cksum_ipv4_verify_host)."""
+    pinned = True
+    try:
+        mi.host_register(host)
+    except Exception:
+        pinned = False
+    mi.ipv4_verify_host(host, n, stride=stride, first_off=first, fixed_len=L)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        _, _, st, bad = mi.ipv4_verify_host(host, n, stride=stride, first_off=first, fixed_len=L)
+    dt = (time.perf_counter() - t0) / iters
+    if pinned:
+        mi.host_unregister(host)
+    assert bad == 0
+    return dict(value=round(n * L / dt / GIB, 2), unit="GiB/s", pinned=pinned,
+                bytes_moved_per_batch=int(host.nbytes), ms_per_batch=round(dt * 1e3, 3))
+
+
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,193 @@
+/*
+ * include/mi_cksum.h -- MI355X-native RFC 1071 Internet checksum: the C ABI.
+ *
+ * libmicksum.so (libunsod_amd/lib/) exports everything declared here.  Plain C,
+ * plain pointers and sizes; no HIP or torch types cross the boundary (streams
+ * are passed as void* hipStream_t, NULL = the default stream).
+ *
+ * Two levels, per SURVEY.md 8(b):
+ *
+ *  (b1) drop-in scalar entry points with the reference's exact names and
+ *       signatures -- they replace the MACHINE_SRCS object in_cksum.o inside
+ *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  Each call
+ *       gathers the mbuf chain into a per-thread pinned staging buffer and runs
+ *       one HIP launch, so a call costs a launch + sync (~10-20 us); the
+ *       bandwidth path is (b2).
+ *
+ *  (b2) batch offload: a batch of packets that already sits in device memory
+ *       (the RX burst / TX inject-ring batch points, uinet_if_dpdk.c:854-879 and
+ *       :360-556) is folded by one kernel launch, asynchronously on `stream`.
+ *
+ * Results are bit-identical to the reference on the same bytes at the same
+ * addresses (address parity matters only for in_cksum_hdr, in_cksum.c:278-285).
+ * There is no CPU fallback: without a usable gfx950 device the batch calls
+ * return -ENODEV and the (b1) calls abort with a message.
+ */
+#ifndef MI_CKSUM_H
+#define MI_CKSUM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* (b1) drop-in entry points -- src/sys/amd64/include/in_cksum.h:44,77-83    */
+/* ------------------------------------------------------------------------ */
+
+/* Only m_next@0, m_data@16 and m_len@24 are read (src/sys/sys/mbuf.h:90-98,
+ * 166-168); the chain is read-only.  struct ip is 20 bytes (netinet/ip.h). */
+struct mbuf;
+struct ip;
+
+/* in_cksum.c:193-232 -- ~fold of bytes [skip, len) of the chain; a short chain
+ * truncates silently; precondition 0 <= skip <= len. */
+unsigned short in_cksum_skip(struct mbuf *m, int len, int skip);
+#define in_cksum(m, len) in_cksum_skip((m), (len), 0)
+
+/* in_cksum.c:241-276 -- L4 verify: pseudo-header (src, dst as loaded from the
+ * header, protonum, (uint16_t)plen) + plen bytes from off0; 0 when valid.
+ * Precondition: the first mbuf holds >= off0 bytes. */
+uint16_t in_cksum_pseudo_header(struct mbuf *m, int plen, int off0, uint32_t src,
+                                uint32_t dst, uint8_t protonum);
+
+/* in_cksum.c:278-285 -- 20-byte IPv4 header, ABSOLUTE-address lanes: at an odd
+ * address the result is byte-swapped relative to in_cksum (SURVEY KAT4). */
+unsigned int in_cksum_hdr(const struct ip *ip);
+
+/* in_cksum.c:181-191 -- non-complemented fold of three u32 (TX seed). */
+unsigned short in_pseudo(unsigned int a, unsigned int b, unsigned int c);
+
+/* in_cksum.c:172-179 -- one's-complement add of two u16. */
+unsigned short in_addword(unsigned short a, unsigned short b);
+
+/* ------------------------------------------------------------------------ */
+/* runtime                                                                    */
+/* ------------------------------------------------------------------------ */
+
+/* Number of HIP devices visible (0 when none / no driver). */
+int mi_cksum_device_count(void);
+/* Bind the calling thread to `device` (hipSetDevice) and create its context.
+ * 0 or -errno (-ENODEV: no such device or not gfx950). */
+int mi_cksum_init(int device);
+/* Text of the last error on this thread ("" if none). */
+const char *mi_cksum_strerror(void);
+const char *mi_cksum_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* (b2) batch offload                                                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * A batch of n packets (or spans) inside one device-resident buffer.
+ *   base      16-byte aligned device pointer; [base, base + roundup16(bytes))
+ *             must be readable (the kernels load whole 16-byte chunks and rely
+ *             on the hardware bounds check of `bytes` for anything beyond).
+ *   bytes     buffer size, < 2^32 - 4096.
+ *   Packet i starts at base + (offs ? offs[i] : first_off + i * stride) and is
+ *   lens[i] (or fixed_len) bytes long.  offs / lens are device arrays.
+ *   max_len   upper bound of lens[] (0 = unknown); sizes the lane groups.
+ * Spans outside [0, bytes) read as zero bytes (hardware bounds check), never
+ * fault.
+ */
+typedef struct mi_pkt_batch {
+	void           *base;
+	uint64_t        bytes;
+	const uint64_t *offs;
+	uint64_t        stride;
+	uint64_t        first_off;
+	const uint32_t *lens;
+	uint32_t        fixed_len;
+	uint32_t        n;
+	uint32_t        max_len;
+	uint32_t        reserved;
+} mi_pkt_batch;
+
+/* Lane conventions for mi_cksum_span_batch. */
+#define MI_SPAN_STREAM 0u  /* in_cksum_skip / in_cksum_pseudo_header: lanes
+                              relative to the span start (in_cksum.c:222-225) */
+#define MI_SPAN_ABS    1u  /* in_cksum_hdr: lanes by absolute address (:278-285) */
+
+/*
+ * Per span: out[i] = ~fold( seed_i + S(span i) ) & 0xffff, where
+ *   seed_i = (seeds ? seeds[i] : 0)
+ *          + (src ? src[i] + dst[i] + (proto[i] << 8) + bswap16(plen_i & 0xffff) : 0)
+ *   plen_i = plens ? plens[i] : span length          (in_cksum.c:252-253)
+ * so MI_SPAN_STREAM with no seeds == in_cksum_skip over a one-mbuf chain, and
+ * with src/dst/proto == in_cksum_pseudo_header(m, plen, off0, ...) where the
+ * span starts at off0.  All arrays are device pointers; out is n u16.
+ */
+typedef struct mi_span_seeds {
+	const uint32_t *seeds;
+	const uint32_t *src;
+	const uint32_t *dst;
+	const uint8_t  *proto;
+	const uint32_t *plens;
+} mi_span_seeds;
+
+int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_seeds *seeds,
+                        uint16_t *out, void *stream);
+
+/* Per-packet status bits (the observable outputs the reference counts:
+ * ips_badsum ip_input.c:469, tcps_rcvbadsum tcp_input.c:717-720). */
+#define MI_ST_IP_BAD    1u
+#define MI_ST_L4_BAD    2u
+#define MI_ST_MALFORMED 4u
+
+/*
+ * RX verify of IPv4 datagrams (ip_input.c:459-471 + tcp_input.c:697-720 /
+ * udp_usrreq.c:440-442), one pass over each datagram.  lens = bytes the NIC
+ * delivered from the IP header on (frame length after Ethernet).
+ *   hl = ip_hl*4, ip_len = ntohs(ip_len)
+ *   flen < 20 || hl < 20 || hl > flen  -> ip = l4 = 0, MALFORMED
+ *   ip = (hl == 20) ? in_cksum_hdr(ip) : in_cksum(m, hl)
+ *   ip_len < hl || ip_len > flen       -> l4 = 0, MALFORMED
+ *   else l4 = in_cksum_pseudo_header(m, ip_len - hl, hl, ip_src, ip_dst, ip_p)
+ * Any output pointer may be NULL.  bad_count (device u32, may be NULL) gains
+ * one per packet with a nonzero status.
+ */
+int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
+                         uint8_t *status, uint32_t *bad_count, void *stream);
+
+/*
+ * TX finalize in place (ip_output.c:649-672 + in_delayed_cksum :958-983):
+ * for TCP/UDP c = in_cksum_skip(m, ip_len, hl) over the pre-seeded L4 header
+ * (UDP: 0 -> 0xffff) stored at hl + (TCP 16 | UDP 6) when inside lens[i]; then
+ * ip_sum = in_cksum(m, hl) with the ip_sum field taken as 0.  Malformed
+ * datagrams (as above) are left untouched.
+ */
+int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream);
+
+/*
+ * Host-resident batch (the path's real start and end: DPDK mbufs in host
+ * memory).  b->base / offs / lens are HOST pointers (page-locked memory gives
+ * full PCIe rate).  The batch is cut into chunks that are copied to device
+ * staging and verified on a ring of streams (H2D || kernel || D2H); outputs
+ * are host arrays.  Synchronous: returns when outputs are written.
+ */
+int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
+                              uint8_t *status, uint32_t *bad_count);
+
+/* Page-lock / unlock a host range for mi_cksum_ipv4_verify_host (hipHostRegister). */
+int mi_cksum_host_register(void *p, uint64_t bytes);
+int mi_cksum_host_unregister(void *p);
+
+/* ------------------------------------------------------------------------ */
+/* workload generator (bench / tests; not part of the reference API)          */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Fill a device batch with synthetic IPv4/TCP datagrams:
+ * payload from splitmix64(seed ^ (byte_index / 8)) over the whole buffer, then
+ * per packet a v4/IHL5 header (ip_len = len, TTL 64, proto 6, DF,
+ * src 10.0.(i>>8).(i&255), dst 10.1.(i>>8).(i&255)) and a 20 B TCP header whose
+ * th_sum holds the in_pseudo seed (tcp_output.c:1063-1085); ip_sum = 0.
+ * Follow with mi_cksum_ipv4_finalize to get valid packets.
+ */
+int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI_CKSUM_H */

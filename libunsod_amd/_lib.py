@@ -1,0 +1,98 @@
+"""Loads libmicksum.so (the HIP extension) and declares the C ABI of
+include/mi_cksum.h for ctypes.
+
+The library is built in-tree (``make -C libunsod_amd/csrc`` or
+``__graft_entry__.build()``) into ``libunsod_amd/lib/libmicksum.so``.  There is no
+fallback: if the library is missing, importing the package raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmicksum.so")
+
+MI_SPAN_STREAM = 0
+MI_SPAN_ABS = 1
+MI_ST_IP_BAD = 1
+MI_ST_L4_BAD = 2
+MI_ST_MALFORMED = 4
+
+
+class MiCksumError(RuntimeError):
+    """A libmicksum batch call returned -errno."""
+
+    def __init__(self, fn: str, rc: int, msg: str):
+        super().__init__(f"{fn} failed ({rc} {os.strerror(-rc) if rc < 0 else ''}): {msg}")
+        self.rc = rc
+
+
+class PktBatchC(C.Structure):
+    """struct mi_pkt_batch (include/mi_cksum.h)."""
+    _fields_ = [
+        ("base", C.c_void_p),
+        ("bytes", C.c_uint64),
+        ("offs", C.c_void_p),
+        ("stride", C.c_uint64),
+        ("first_off", C.c_uint64),
+        ("lens", C.c_void_p),
+        ("fixed_len", C.c_uint32),
+        ("n", C.c_uint32),
+        ("max_len", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class SpanSeedsC(C.Structure):
+    """struct mi_span_seeds (include/mi_cksum.h)."""
+    _fields_ = [(k, C.c_void_p) for k in ("seeds", "src", "dst", "proto", "plens")]
+
+
+# Every symbol include/mi_cksum.h declares -> (restype, argtypes).
+SIGNATURES = {
+    "in_cksum_skip": (C.c_ushort, [C.c_void_p, C.c_int, C.c_int]),
+    "in_cksum_pseudo_header": (C.c_uint16, [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.c_uint8]),
+    "in_cksum_hdr": (C.c_uint, [C.c_void_p]),
+    "in_pseudo": (C.c_ushort, [C.c_uint, C.c_uint, C.c_uint]),
+    "in_addword": (C.c_ushort, [C.c_ushort, C.c_ushort]),
+    "mi_cksum_device_count": (C.c_int, []),
+    "mi_cksum_init": (C.c_int, [C.c_int]),
+    "mi_cksum_strerror": (C.c_char_p, []),
+    "mi_cksum_version": (C.c_char_p, []),
+    "mi_cksum_span_batch": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(SpanSeedsC), C.c_void_p,
+                                      C.c_void_p]),
+    "mi_cksum_ipv4_verify": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                       C.c_void_p]),
+    "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
+    "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p]),
+    "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "mi_cksum_host_unregister": (C.c_int, [C.c_void_p]),
+    "mi_cksum_synth_ipv4": (C.c_int, [C.POINTER(PktBatchC), C.c_uint64, C.c_void_p]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libmicksum.so once; raise if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: the HIP extension must be built "
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C libunsod_amd/csrc)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(fn: str, rc: int) -> None:
+    if rc != 0:
+        raise MiCksumError(fn, rc, load().mi_cksum_strerror().decode(errors="replace"))

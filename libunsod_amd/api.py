@@ -1,0 +1,223 @@
+"""Python mirror of the reference checksum interface, over the C ABI.
+
+Scalar layer -- same names, argument meaning and (lack of) error behaviour as
+src/sys/amd64/include/in_cksum.h:44,77-83.  ``MbufChain`` builds a real
+``struct mbuf`` chain in host memory (256 B mbufs; m_next@0, m_data@16,
+m_len@24 as in src/sys/sys/mbuf.h:90-98,166-168) so the calls below go through
+libmicksum's drop-in C symbols exactly as libuinet's protocol code would.
+
+Batch layer -- ``PktBatch`` describes packets in a device-resident torch uint8
+tensor; ``ipv4_verify`` / ``ipv4_finalize`` / ``span_batch`` launch the gfx950
+kernels on the current torch stream (asynchronous).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable
+
+import numpy as np
+
+from ._lib import (MI_SPAN_ABS, MI_SPAN_STREAM, PktBatchC, SpanSeedsC, check, load)
+
+MSIZE = 256  # param.h:159
+
+
+# ----------------------------------------------------------------- scalar (b1)
+class MbufChain:
+    """A chain of real mbufs over ``segments``.
+
+    Each segment is ``bytes`` or ``(bytes, addr_mod)``; the data of a segment is
+    placed at an address == addr_mod (mod 64) -- address parity is what the
+    reference's per-span swap (in_cksum.c:222-225) reacts to.
+    """
+
+    def __init__(self, segments: Iterable):
+        segs = [(s, 0) if isinstance(s, (bytes, bytearray, memoryview, np.ndarray)) else s for s in segments]
+        if not segs:
+            raise ValueError("an mbuf chain has at least one mbuf")
+        self._keep = []
+        self.mbufs = np.zeros(len(segs) * MSIZE + 64, np.uint8)
+        mb_base = self.mbufs.ctypes.data + ((-self.mbufs.ctypes.data) % 64)
+        addrs = [mb_base + k * MSIZE for k in range(len(segs))]
+        for k, (data, mod) in enumerate(segs):
+            raw = np.frombuffer(bytes(data), np.uint8)
+            buf = np.zeros(raw.size + 192, np.uint8)
+            start = 64 + ((mod - (buf.ctypes.data + 64)) % 64)
+            buf[start:start + raw.size] = raw
+            self._keep.append(buf)
+            nxt = addrs[k + 1] if k + 1 < len(segs) else 0
+            C.c_uint64.from_address(addrs[k]).value = nxt                   # m_next
+            C.c_uint64.from_address(addrs[k] + 16).value = buf.ctypes.data + start  # m_data
+            C.c_int32.from_address(addrs[k] + 24).value = raw.size           # m_len
+        self.ptr = addrs[0]
+        self.total = sum(len(bytes(d)) for d, _ in segs)
+
+
+def in_cksum_skip(m: MbufChain, length: int, skip: int) -> int:
+    return int(load().in_cksum_skip(C.c_void_p(m.ptr), length, skip))
+
+
+def in_cksum(m: MbufChain, length: int) -> int:
+    return in_cksum_skip(m, length, 0)
+
+
+def in_cksum_pseudo_header(m: MbufChain, plen: int, off0: int, src: int, dst: int, protonum: int) -> int:
+    return int(load().in_cksum_pseudo_header(C.c_void_p(m.ptr), plen, off0, src & 0xFFFFFFFF,
+                                             dst & 0xFFFFFFFF, protonum & 0xFF))
+
+
+def in_cksum_hdr(ip, addr_mod: int = 0) -> int:
+    """``ip``: 20 header bytes, placed at an address == addr_mod (mod 64)."""
+    raw = np.frombuffer(bytes(ip), np.uint8)
+    buf = np.zeros(256, np.uint8)
+    start = 64 + ((addr_mod - (buf.ctypes.data + 64)) % 64)
+    buf[start:start + raw.size] = raw
+    return int(load().in_cksum_hdr(C.c_void_p(buf.ctypes.data + start)))
+
+
+def in_pseudo(a: int, b: int, c: int) -> int:
+    return int(load().in_pseudo(a & 0xFFFFFFFF, b & 0xFFFFFFFF, c & 0xFFFFFFFF))
+
+
+def in_addword(a: int, b: int) -> int:
+    return int(load().in_addword(a & 0xFFFF, b & 0xFFFF))
+
+
+# ------------------------------------------------------------------ batch (b2)
+def _torch():
+    import torch  # deferred: the scalar layer needs no torch
+    return torch
+
+
+def _stream(stream) -> int:
+    torch = _torch()
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+class PktBatch:
+    """n packets in a device uint8 tensor ``buf``.
+
+    Packet i starts at ``offs[i]`` (device int64 tensor) or
+    ``first_off + i*stride`` and is ``lens[i]`` (device int32 tensor) or
+    ``fixed_len`` bytes long.
+    """
+
+    def __init__(self, buf, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
+                 fixed_len: int = 0, max_len: int = 0):
+        torch = _torch()
+        if buf.dtype != torch.uint8 or not buf.is_contiguous():
+            raise ValueError("buf must be a contiguous uint8 tensor")
+        self.buf, self.n = buf, int(n)
+        self.offs = None if offs is None else offs.to(torch.int64).contiguous()
+        self.lens = None if lens is None else lens.to(torch.int32).contiguous()
+        self.stride, self.first_off, self.fixed_len = int(stride), int(first_off), int(fixed_len)
+        self.max_len = int(max_len)
+        if self.lens is not None and not self.max_len:
+            self.max_len = int(self.lens.max().item()) if self.n else 0
+        self._c = PktBatchC(buf.data_ptr(), buf.numel(),
+                            self.offs.data_ptr() if self.offs is not None else None,
+                            self.stride, self.first_off,
+                            self.lens.data_ptr() if self.lens is not None else None,
+                            self.fixed_len, self.n, self.max_len, 0)
+
+    @property
+    def c(self) -> PktBatchC:
+        return self._c
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def ipv4_verify(b: PktBatch, *, ip: bool = True, l4: bool = True, status: bool = True,
+                bad_count: bool = False, out=None, stream=None) -> dict:
+    """RX verify (ip_input.c:459-471 + tcp_input.c:697-720).  Returns a dict of
+    device tensors: ip / l4 (uint16), status (uint8), bad (int32[1], a u32 count)."""
+    torch = _torch()
+    dev = b.buf.device
+    res = dict(out or {})
+    if ip and "ip" not in res:
+        res["ip"] = torch.empty(b.n, dtype=torch.uint16, device=dev)
+    if l4 and "l4" not in res:
+        res["l4"] = torch.empty(b.n, dtype=torch.uint16, device=dev)
+    if status and "status" not in res:
+        res["status"] = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    if bad_count:
+        res["bad"] = res.get("bad", torch.zeros(1, dtype=torch.int32, device=dev))
+        res["bad"].zero_()
+    check("mi_cksum_ipv4_verify",
+          load().mi_cksum_ipv4_verify(C.byref(b.c), _ptr(res.get("ip")), _ptr(res.get("l4")),
+                                      _ptr(res.get("status")), _ptr(res.get("bad")),
+                                      C.c_void_p(_stream(stream))))
+    return res
+
+
+def ipv4_finalize(b: PktBatch, stream=None) -> None:
+    """TX finalize in place (in_delayed_cksum ip_output.c:958-983 + ip_sum :667-672)."""
+    check("mi_cksum_ipv4_finalize", load().mi_cksum_ipv4_finalize(C.byref(b.c), C.c_void_p(_stream(stream))))
+
+
+def span_batch(b: PktBatch, lanes: int = MI_SPAN_STREAM, *, seeds=None, src=None, dst=None, proto=None,
+               plens=None, out=None, stream=None):
+    """Per-span ~fold(seed + S(span)) -- in_cksum_skip / in_cksum_pseudo_header /
+    in_cksum_hdr (lanes=MI_SPAN_ABS) over one-mbuf spans."""
+    torch = _torch()
+    out = torch.empty(b.n, dtype=torch.uint16, device=b.buf.device) if out is None else out
+    keep = [None if x is None else x.contiguous() for x in (seeds, src, dst, proto, plens)]
+    s = SpanSeedsC(*[_ptr(x) for x in keep])
+    check("mi_cksum_span_batch",
+          load().mi_cksum_span_batch(C.byref(b.c), lanes, C.byref(s), out.data_ptr(), C.c_void_p(_stream(stream))))
+    return out
+
+
+def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
+    """Device-side workload generator (not part of the reference API)."""
+    check("mi_cksum_synth_ipv4", load().mi_cksum_synth_ipv4(C.byref(b.c), seed, C.c_void_p(_stream(stream))))
+
+
+def ipv4_verify_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
+                     fixed_len: int = 0):
+    """Host-resident batch: chunked H2D -> verify -> D2H.  Returns numpy
+    (ip, l4, status, bad_count).  Page-lock ``buf`` (host_register) for full
+    PCIe rate."""
+    offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
+    lens = None if lens is None else np.ascontiguousarray(lens, np.uint32)
+    hb = PktBatchC(buf.ctypes.data, buf.nbytes, None if offs is None else offs.ctypes.data, stride, first_off,
+                   None if lens is None else lens.ctypes.data, fixed_len, n,
+                   int(lens.max()) if lens is not None and n else fixed_len, 0)
+    ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
+    bad = C.c_uint32(0)
+    check("mi_cksum_ipv4_verify_host",
+          load().mi_cksum_ipv4_verify_host(C.byref(hb), ip.ctypes.data, l4.ctypes.data, st.ctypes.data,
+                                           C.addressof(bad)))
+    return ip, l4, st, int(bad.value)
+
+
+def host_register(buf: np.ndarray) -> None:
+    check("mi_cksum_host_register", load().mi_cksum_host_register(buf.ctypes.data, buf.nbytes))
+
+
+def host_unregister(buf: np.ndarray) -> None:
+    check("mi_cksum_host_unregister", load().mi_cksum_host_unregister(buf.ctypes.data))
+
+
+def init(device: int = 0) -> None:
+    check("mi_cksum_init", load().mi_cksum_init(device))
+
+
+def device_count() -> int:
+    return int(load().mi_cksum_device_count())
+
+
+def version() -> str:
+    return load().mi_cksum_version().decode()
+
+
+__all__ = [
+    "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
+    "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
+    "ipv4_verify_host", "host_register", "host_unregister", "init", "device_count", "version",
+    "MI_SPAN_STREAM", "MI_SPAN_ABS",
+]

@@ -1,0 +1,841 @@
+// libunsod_amd/csrc/cksum_kernels.hip -- CDNA4 (gfx950) kernels and the HIP
+// runtime behind include/mi_cksum.h.
+//
+// The hot path is an integer fold bound by HBM read bandwidth (~1 add per 4 B,
+// SURVEY.md 8(d)); no MFMA.  Design:
+//
+//  * A packet is folded by a LANE GROUP of G = 4..64 lanes (G sized on the host
+//    from the longest packet so that a lane owns <= U = 4 chunks per pass).
+//    Lane j of a group loads the 16-byte chunks j, j+G, j+2G, ... of the
+//    16-byte-aligned envelope of the packet: every wave-instruction is a fully
+//    coalesced buffer_load_dwordx4 of up to 1 KiB, and a lane keeps U of them in
+//    flight (U x 16 B x 64 lanes x 8 waves/SIMD = up to 128 KiB per CU).
+//  * Loads go through a buffer resource (T8/T20) built from kernel arguments:
+//    32-bit offsets, hardware bounds check on `bytes`.  Chunks past a packet's
+//    end get an out-of-range offset, so they cost no memory traffic, and a bad
+//    descriptor can never fault the GPU.
+//  * Bytes outside the packet (envelope head/tail) are masked per dword.  Each
+//    dword w is accumulated as (w & 0xffff) + (w >> 16) into a u32 -- the
+//    absolute-address 16-bit lanes of in_cksumdata (in_cksum.c:91-170) -- and
+//    folded once per pass, so any packet length is overflow-safe.
+//  * The group's partial sums meet in a __shfl_xor butterfly (ds_bpermute,
+//    64-wide wave); the group leader folds, applies the stream-parity swap
+//    (in_cksum.c:222-225), adds the pseudo-header seed (:252-253), folds and
+//    complements.  No atomics on the data path, results are deterministic.
+//  * The IPv4 header fields (hl, ip_len, proto, src, dst) are read from the
+//    first three chunks that lanes 0..2 of the group already hold (group
+//    broadcast), so the header costs no extra memory instruction.
+//
+// Bit-exactness: the fold is the end-around-carry sum mod 65535 that is zero
+// only for an all-zero input, the same equivalence class REDUCE16 yields, so
+// the association order (lanes, passes, butterfly) cannot change the result.
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mi_cksum.h"
+#include "mi_internal.h"
+
+#define MI_CKSUM_VERSION "libmicksum 0.1 (gfx950)"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+constexpr int kBlock = 256;           // 4 waves
+constexpr int kU = 4;                 // chunks per lane per pass
+constexpr uint32_t kOOB = 0xFFFFF000u;  // offset the bounds check always rejects
+constexpr uint64_t kMaxBytes = 0xFFFFF000ull - 4096;
+
+// ---------------------------------------------------------------- device math
+__device__ __forceinline__ uint32_t fold16(uint32_t x) {
+  x = (x & 0xffffu) + (x >> 16);
+  x = (x & 0xffffu) + (x >> 16);
+  return x;
+}
+__device__ __forceinline__ uint32_t fold16_64(uint64_t s) {
+  s = (s & 0xffffffffull) + (s >> 32);
+  s = (s & 0xffffffffull) + (s >> 32);
+  return fold16((uint32_t)s);
+}
+__device__ __forceinline__ uint32_t swap16(uint32_t x) {
+  return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
+}
+// Mask of the bytes [lo, hi) (relative to a 16-byte chunk) inside dword k.
+__device__ __forceinline__ uint32_t dmask(int lo, int hi, int k) {
+  const int a = min(max(lo - 4 * k, 0), 4);
+  const int b = min(max(hi - 4 * k, 0), 4);
+  const uint32_t mb = b >= 4 ? 0xffffffffu : ((1u << (8 * b)) - 1u);
+  const uint32_t ma = a >= 4 ? 0xffffffffu : ((1u << (8 * a)) - 1u);
+  return mb & ~ma;
+}
+__device__ __forceinline__ uint32_t halves(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+
+// Sum of the bytes of chunk v that fall in [r0, r1) relative to the packet
+// start, where the chunk starts at `rel` relative to the packet start.
+__device__ __forceinline__ uint32_t chunk_range_sum(const u32x4 &v, int rel, int r0, int r1) {
+  const int lo = min(max(r0 - rel, 0), 16);
+  const int hi = min(max(r1 - rel, 0), 16);
+  if (lo >= hi) return 0u;
+  if (lo == 0 && hi == 16) return halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+  return halves(v.x & dmask(lo, hi, 0)) + halves(v.y & dmask(lo, hi, 1)) +
+         halves(v.z & dmask(lo, hi, 2)) + halves(v.w & dmask(lo, hi, 3));
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+#pragma unroll
+  for (int o = G / 2; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
+// Value of lane k (0..2) of this lane's group.
+template <int G>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t x, int k) {
+  if constexpr (G == 64) {
+    return __builtin_amdgcn_readlane(x, k);
+  } else {
+    return __shfl(x, (int)(threadIdx.x & 63u & ~(unsigned)(G - 1)) + k, 64);
+  }
+}
+
+struct Desc {
+  const uint8_t *base;
+  uint32_t bytes;  // bounds-check size (rounded up to 16)
+  uint32_t n;
+  const uint64_t *offs;
+  uint64_t stride, first_off;
+  const uint32_t *lens;
+  uint32_t fixed_len;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(d.base), 0, (int)d.bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ uint32_t pkt_off(const Desc &d, uint32_t i) {
+  const uint64_t o = d.offs ? d.offs[i] : d.first_off + (uint64_t)i * d.stride;
+  return o < kOOB ? (uint32_t)o : kOOB;
+}
+__device__ __forceinline__ uint32_t pkt_len(const Desc &d, uint32_t i) {
+  const uint32_t l = d.lens ? d.lens[i] : d.fixed_len;
+  return l < 0x7fff0000u ? l : 0x7fff0000u;
+}
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
+// Issue the kU loads of pass p for a packet whose envelope starts at chunk c0
+// and has nch chunks.
+template <int G>
+__device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0, uint32_t nch,
+                                           uint32_t p, int lane, u32x4 (&v)[kU]) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const uint32_t ci = p * (G * kU) + u * G + lane;
+    v[u] = ld16(r, ci < nch ? c0 + 16u * ci : kOOB);
+  }
+}
+
+// Header fields of an IPv4 datagram starting h bytes into chunk 0, read from
+// chunks 0..2 held by lanes 0..2 of the group (pass 0, u = 0).
+struct IpHdr {
+  uint32_t hl, iplen, proto, src, dst;
+};
+template <int G>
+__device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
+  uint32_t D[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    D[4 * c + 0] = group_bcast<G>(v0.x, c);
+    D[4 * c + 1] = group_bcast<G>(v0.y, c);
+    D[4 * c + 2] = group_bcast<G>(v0.z, c);
+    D[4 * c + 3] = group_bcast<G>(v0.w, c);
+  }
+  const uint32_t q = h >> 2, rb = h & 3u;
+  uint32_t T[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+    T[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
+  // little-endian u32 at byte h + 4k = alignbyte({T[k+1], T[k]}, rb)
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(T[1], T[0], rb);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(T[3], T[2], rb);
+  IpHdr ih;
+  ih.hl = (w0 & 0x0fu) << 2;
+  ih.iplen = ((w0 >> 8) & 0xff00u) | (w0 >> 24);
+  ih.proto = (w2 >> 8) & 0xffu;
+  ih.src = __builtin_amdgcn_alignbyte(T[4], T[3], rb);
+  ih.dst = __builtin_amdgcn_alignbyte(T[5], T[4], rb);
+  return ih;
+}
+
+// ------------------------------------------------------------------ kernels
+
+// Generic spans: in_cksum_skip / in_cksum_pseudo_header / in_cksum_hdr.
+struct SpanSeeds {
+  const uint32_t *seeds, *src, *dst;
+  const uint8_t *proto;
+  const uint32_t *plens;
+};
+
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, SpanSeeds s,
+                                                 uint16_t *out) {
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
+    const uint32_t off = pkt_off(d, i), len = pkt_len(d, i);
+    const uint32_t c0 = off & ~15u, h = off & 15u;
+    const uint32_t nch = len ? (h + len + 15u) >> 4 : 0u;
+    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+    uint32_t acc = 0;
+    for (uint32_t p = 0; p < npass; ++p) {
+      u32x4 v[kU];
+      issue_pass<G>(r, c0, nch, p, lane, v);
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+        acc += chunk_range_sum(v[u], rel, 0, (int)len);
+      }
+      acc = fold16(acc);
+    }
+    acc = group_sum<G>(acc);
+    if (lane == 0) {
+      uint64_t sum = fold16(acc);
+      if (!abs_lanes && (((uintptr_t)d.base + off) & 1u)) sum = swap16((uint32_t)sum);
+      if (s.seeds) sum += s.seeds[i];
+      if (s.src) {
+        const uint32_t pl = s.plens ? s.plens[i] : len;
+        sum += (uint64_t)s.src[i] + s.dst[i] + ((uint32_t)s.proto[i] << 8) + swap16(pl & 0xffffu);
+      }
+      out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+    }
+  }
+}
+
+// RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
+                                                        uint16_t *l4_out, uint8_t *st_out,
+                                                        uint32_t *bad) {
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
+    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    const uint32_t c0 = off & ~15u, h = off & 15u;
+    const uint32_t nch = (h + flen + 15u) >> 4;
+    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+
+    u32x4 v[kU];
+    issue_pass<G>(r, c0, nch, 0, lane, v);
+    const IpHdr ih = parse_ipv4<G>(v[0], h);
+    const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+    const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+    const int hend = hdr_ok ? (int)ih.hl : 0;
+    const int lend = l4_ok ? (int)ih.iplen : hend;
+
+    uint32_t acc_h = 0, acc_l = 0;
+    for (uint32_t p = 0;;) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+        acc_h += chunk_range_sum(v[u], rel, 0, hend);
+        acc_l += chunk_range_sum(v[u], rel, hend, lend);
+      }
+      acc_l = fold16(acc_l);
+      if (++p >= npass) break;
+      issue_pass<G>(r, c0, nch, p, lane, v);
+    }
+    acc_h = group_sum<G>(fold16(acc_h));
+    acc_l = group_sum<G>(acc_l);
+    if (lane == 0) {
+      const bool odd = ((uintptr_t)d.base + off) & 1u;
+      uint32_t ip = 0, l4 = 0, st = 0;
+      if (!hdr_ok) {
+        st = MI_ST_MALFORMED;
+      } else {
+        uint32_t sh = fold16(acc_h);
+        if (ih.hl != 20u && odd) sh = swap16(sh);  // in_cksum (stream) vs in_cksum_hdr (abs)
+        ip = ~sh & 0xffffu;
+        if (l4_ok) {
+          uint32_t sl = fold16(acc_l);
+          if (odd) sl = swap16(sl);
+          const uint32_t plen = ih.iplen - ih.hl;
+          const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(plen);
+          l4 = ~fold16_64(seed + sl) & 0xffffu;
+        } else {
+          st = MI_ST_MALFORMED;
+        }
+        st |= (ip ? MI_ST_IP_BAD : 0u) | (l4 ? MI_ST_L4_BAD : 0u);
+      }
+      if (ip_out) ip_out[i] = (uint16_t)ip;
+      if (l4_out) l4_out[i] = (uint16_t)l4;
+      if (st_out) st_out[i] = (uint8_t)st;
+      if (bad && st) atomicAdd(bad, 1u);
+    }
+  }
+}
+
+// TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
+// (ip_output.c:667-672).
+template <int G>
+__global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
+    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    const uint32_t c0 = off & ~15u, h = off & 15u;
+    const uint32_t nch = (h + flen + 15u) >> 4;
+    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+
+    u32x4 v[kU];
+    issue_pass<G>(r, c0, nch, 0, lane, v);
+    const IpHdr ih = parse_ipv4<G>(v[0], h);
+    const bool ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl &&
+                    ih.iplen <= flen;
+    const bool do_l4 = ok && (ih.proto == 6u || ih.proto == 17u);
+    const int hend = ok ? (int)ih.hl : 0;
+    const int lend = do_l4 ? (int)ih.iplen : hend;
+
+    uint32_t acc_h = 0, acc_l = 0;
+    for (uint32_t p = 0;;) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+        // ip_sum (bytes 10..11) is zeroed before in_cksum (ip_output.c:670-672)
+        acc_h += chunk_range_sum(v[u], rel, 0, min(hend, 10)) +
+                 chunk_range_sum(v[u], rel, 12, hend);
+        acc_l += chunk_range_sum(v[u], rel, hend, lend);
+      }
+      acc_l = fold16(acc_l);
+      if (++p >= npass) break;
+      issue_pass<G>(r, c0, nch, p, lane, v);
+    }
+    acc_h = group_sum<G>(fold16(acc_h));
+    acc_l = group_sum<G>(acc_l);
+    if (lane == 0 && ok) {
+      const bool odd = ((uintptr_t)d.base + off) & 1u;
+      if (do_l4) {
+        uint32_t sl = fold16(acc_l);
+        if (odd) sl = swap16(sl);
+        uint32_t c = ~sl & 0xffffu;
+        if (ih.proto == 17u && c == 0u) c = 0xffffu;
+        const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
+        if (at + 2u <= flen) {
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+        }
+      }
+      uint32_t sh = fold16(acc_h);
+      if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
+      const uint32_t c = ~sh & 0xffffu;
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + 11u, 0, 0);
+    }
+  }
+}
+
+// ---------------------------------------------------------- workload generator
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void k_fill(uint8_t *base, uint64_t bytes, uint64_t seed) {
+  const uint64_t nchunk = bytes / 16;
+  for (uint64_t c = blockIdx.x * (uint64_t)kBlock + threadIdx.x; c < nchunk;
+       c += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t a = splitmix64(seed ^ (2 * c)), b = splitmix64(seed ^ (2 * c + 1));
+    u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+    *reinterpret_cast<u32x4 *>(base + 16 * c) = v;
+  }
+}
+
+__device__ __forceinline__ void put_be16(uint8_t *p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_synth_hdr(Desc d) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= d.n) return;
+  const uint64_t off = d.offs ? d.offs[i] : d.first_off + (uint64_t)i * d.stride;
+  const uint32_t len = d.lens ? d.lens[i] : d.fixed_len;
+  if (len < 40u || off + 40u > d.bytes) return;
+  uint8_t *p = const_cast<uint8_t *>(d.base) + off;
+  p[0] = 0x45; p[1] = 0;
+  put_be16(p + 2, len);
+  put_be16(p + 4, i & 0xffffu);
+  put_be16(p + 6, 0x4000);
+  p[8] = 64; p[9] = 6; p[10] = 0; p[11] = 0;
+  p[12] = 10; p[13] = 0; p[14] = (uint8_t)(i >> 8); p[15] = (uint8_t)i;
+  p[16] = 10; p[17] = 1; p[18] = (uint8_t)(i >> 8); p[19] = (uint8_t)i;
+  uint8_t *t = p + 20;
+  put_be16(t + 0, 40000u + (i % 1000u));
+  put_be16(t + 2, 5201);
+  put_be16(t + 4, i >> 16); put_be16(t + 6, i);  // seq
+  put_be16(t + 8, 0); put_be16(t + 10, 1);       // ack
+  t[12] = 5 << 4; t[13] = 0x10;
+  put_be16(t + 14, 65535);
+  // th_sum = in_pseudo(src, dst, htons(tcp_len + IPPROTO_TCP)) (tcp_output.c:1084)
+  const uint32_t src = 10u | (0u << 8) | ((i >> 8) & 0xffu) << 16 | (i & 0xffu) << 24;
+  const uint32_t dst = 10u | (1u << 8) | ((i >> 8) & 0xffu) << 16 | (i & 0xffu) << 24;
+  const uint32_t seed = fold16_64((uint64_t)src + dst + swap16((len - 20u + 6u) & 0xffffu));
+  t[16] = (uint8_t)seed; t[17] = (uint8_t)(seed >> 8);
+  t[18] = 0; t[19] = 0;
+}
+
+// Scalar drop-in path: one span in page-locked host memory (read over PCIe).
+__global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
+                                               uint32_t len, uint32_t abs_lanes, int pseudo,
+                                               uint32_t src, uint32_t dst, uint32_t proto,
+                                               uint32_t plen, uint16_t *out) {
+  Desc d{};
+  d.base = base; d.bytes = bytes; d.n = 1; d.first_off = off; d.fixed_len = len;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  constexpr int G = 64;
+  const int lane = threadIdx.x;
+  const uint32_t c0 = off & ~15u, h = off & 15u;
+  const uint32_t nch = len ? (h + len + 15u) >> 4 : 0u;
+  const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+  uint32_t acc = 0;
+  for (uint32_t p = 0; p < npass; ++p) {
+    u32x4 v[kU];
+    issue_pass<G>(r, c0, nch, p, lane, v);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+      acc += chunk_range_sum(v[u], rel, 0, (int)len);
+    }
+    acc = fold16(acc);
+  }
+  acc = group_sum<G>(acc);
+  if (lane == 0) {
+    uint64_t sum = fold16(acc);
+    if (!abs_lanes && (((uintptr_t)base + off) & 1u)) sum = swap16((uint32_t)sum);
+    if (pseudo) sum += (uint64_t)src + dst + (proto << 8) + swap16(plen & 0xffffu);
+    *out = (uint16_t)(~fold16_64(sum) & 0xffffu);
+  }
+}
+
+// ------------------------------------------------------------------- runtime
+thread_local char t_err[256];
+
+int set_err(int code, const char *fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(t_err, sizeof t_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return set_err(-EIO, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__,  \
+                     __LINE__);                                                        \
+  } while (0)
+
+struct ThreadCtx {
+  int device = -1;
+  // scalar (b1) path
+  hipStream_t sstream = nullptr;
+  uint8_t *stage = nullptr;  // page-locked, device-mapped
+  size_t stage_cap = 0;
+  uint16_t *sout = nullptr;  // page-locked result slot
+  // host-batch path
+  static constexpr int kRing = 3;
+  hipStream_t hstream[kRing] = {};
+  uint8_t *dstage[kRing] = {};
+  uint16_t *dout[kRing] = {};   // ip, l4 pairs
+  uint8_t *dst8[kRing] = {};
+  uint8_t *ddesc[kRing] = {};  // rebased offs (u64) + lens (u32), device
+  uint8_t *hdesc[kRing] = {};  // same, page-locked host
+  uint32_t *dbad = nullptr;
+  size_t dstage_cap = 0, dout_cap = 0;
+};
+thread_local ThreadCtx t_ctx;
+
+int check_device(int dev) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return set_err(-ENODEV, "device %d is %s, not gfx950", dev, prop.gcnArchName);
+  return 0;
+}
+
+// Make sure the calling thread has a context on its current HIP device.
+int ensure_ctx() {
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return set_err(-ENODEV, "no HIP device: %s", hipGetErrorString(e));
+  if (t_ctx.device == dev) return 0;
+  int rc = check_device(dev);
+  if (rc) return rc;
+  if (t_ctx.device != -1) {
+    // thread moved to another device: start a fresh context (old one leaks by design;
+    // its streams belong to the other device)
+    t_ctx = ThreadCtx();
+  }
+  t_ctx.device = dev;
+  return 0;
+}
+
+int pick_group(uint32_t max_len) {
+  // chunks of the 16-byte envelope, worst-case misalignment
+  const uint32_t ch = (max_len + 15u + 15u) / 16u;
+  const uint32_t per = (ch + kU - 1) / kU;
+  if (per <= 4) return 4;
+  if (per <= 8) return 8;
+  if (per <= 16) return 16;
+  if (per <= 32) return 32;
+  return 64;
+}
+
+int grid_for(uint32_t n, int G) {
+  static int cap = [] {
+    const char *s = getenv("MI_CKSUM_MAX_BLOCKS");
+    int v = s ? atoi(s) : 0;
+    return v > 0 ? v : 4096;
+  }();
+  const uint64_t groups_per_block = kBlock / G;
+  uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
+  if (blocks > (uint64_t)cap) blocks = cap;
+  return blocks ? (int)blocks : 1;
+}
+
+int make_desc(const mi_pkt_batch *b, Desc *d) {
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (((uintptr_t)b->base & 15u) != 0) return set_err(-EINVAL, "base %p not 16-byte aligned", b->base);
+  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "batch buffer %llu B >= 4 GiB", (unsigned long long)b->bytes);
+  if (b->n && !b->base) return set_err(-EINVAL, "base is NULL");
+  if (!b->offs && b->n) {
+    const uint64_t last = b->first_off + (uint64_t)(b->n - 1) * b->stride;
+    if (!b->lens && last + b->fixed_len > b->bytes)
+      return set_err(-ERANGE, "packet %u ends at %llu > bytes %llu", b->n - 1,
+                     (unsigned long long)(last + b->fixed_len), (unsigned long long)b->bytes);
+  }
+  d->base = (const uint8_t *)b->base;
+  d->bytes = (uint32_t)((b->bytes + 15u) & ~15ull);
+  d->n = b->n;
+  d->offs = b->offs;
+  d->stride = b->stride;
+  d->first_off = b->first_off;
+  d->lens = b->lens;
+  d->fixed_len = b->fixed_len;
+  return 0;
+}
+
+uint32_t batch_max_len(const mi_pkt_batch *b) {
+  if (!b->lens) return b->fixed_len;
+  return b->max_len ? b->max_len : 1500u;
+}
+
+#define DISPATCH_G(G, CALL)                 \
+  switch (G) {                              \
+    case 4: { constexpr int kG = 4; CALL; } break;   \
+    case 8: { constexpr int kG = 8; CALL; } break;   \
+    case 16: { constexpr int kG = 16; CALL; } break; \
+    case 32: { constexpr int kG = 32; CALL; } break; \
+    default: { constexpr int kG = 64; CALL; } break; \
+  }
+
+int launch_verify(const Desc &d, int G, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad,
+                  hipStream_t s) {
+  const int grid = grid_for(d.n, G);
+  DISPATCH_G(G, hipLaunchKernelGGL(k_ipv4_verify<kG>, dim3(grid), dim3(kBlock), 0, s, d, ip, l4, st, bad));
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI
+extern "C" {
+
+const char *mi_cksum_version(void) { return MI_CKSUM_VERSION; }
+const char *mi_cksum_strerror(void) { return t_err; }
+
+int mi_cksum_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int mi_cksum_init(int device) {
+  int n = mi_cksum_device_count();
+  if (device < 0 || device >= n) return set_err(-ENODEV, "device %d of %d", device, n);
+  HIP_TRY(hipSetDevice(device));
+  return ensure_ctx();
+}
+
+int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_seeds *seeds,
+                        uint16_t *out, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  if (!d.n) return 0;
+  if (!out) return set_err(-EINVAL, "out is NULL");
+  SpanSeeds s{};
+  if (seeds) {
+    s.seeds = seeds->seeds; s.src = seeds->src; s.dst = seeds->dst;
+    s.proto = seeds->proto; s.plens = seeds->plens;
+    if (s.src && (!s.dst || !s.proto)) return set_err(-EINVAL, "src without dst/proto");
+  }
+  const int G = pick_group(batch_max_len(b));
+  const int grid = grid_for(d.n, G);
+  const uint32_t abs_lanes = lanes == MI_SPAN_ABS;
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_G(G, hipLaunchKernelGGL(k_span<kG>, dim3(grid), dim3(kBlock), 0, st, d, abs_lanes, s, out));
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
+                         uint8_t *status, uint32_t *bad_count, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  if (!d.n) return 0;
+  return launch_verify(d, pick_group(batch_max_len(b)), ip_sum, l4_sum, status, bad_count,
+                       (hipStream_t)stream);
+}
+
+int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  if (!d.n) return 0;
+  const int G = pick_group(batch_max_len(b));
+  const int grid = grid_for(d.n, G);
+  hipStream_t st = (hipStream_t)stream;
+  DISPATCH_G(G, hipLaunchKernelGGL(k_ipv4_finalize<kG>, dim3(grid), dim3(kBlock), 0, st, d));
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  d.bytes = (uint32_t)b->bytes;  // header writes stay inside the real buffer
+  const uint64_t fill = b->bytes & ~15ull;
+  if (fill) {
+    uint64_t blocks = (fill / 16 + kBlock - 1) / kBlock;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(kBlock), 0, st, (uint8_t *)b->base, fill, seed);
+    HIP_TRY(hipGetLastError());
+  }
+  if (d.n) {
+    hipLaunchKernelGGL(k_synth_hdr, dim3((d.n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, d);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
+}
+
+int mi_cksum_host_register(void *p, uint64_t bytes) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return 0;
+}
+
+int mi_cksum_host_unregister(void *p) {
+  HIP_TRY(hipHostUnregister(p));
+  return 0;
+}
+
+// Host-resident batch: chunked H2D -> verify -> D2H on a ring of streams, so the
+// copy of chunk k+1 overlaps the kernel of chunk k (PCIe-bound).
+int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
+                              uint8_t *status, uint32_t *bad_count) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (bad_count) *bad_count = 0;
+  if (!b->n) return 0;
+  if (!b->base) return set_err(-EINVAL, "base is NULL");
+  ThreadCtx &c = t_ctx;
+  static const uint64_t kChunk = [] {
+    const char *s = getenv("MI_CKSUM_HOST_CHUNK");
+    long long v = s ? atoll(s) : 0;
+    return (uint64_t)(v > 0 ? v : (8ll << 20));
+  }();
+  const uint8_t *hb = (const uint8_t *)b->base;
+  const bool var = b->offs || b->lens;
+  auto off_of = [&](uint32_t i) { return b->offs ? b->offs[i] : b->first_off + (uint64_t)i * b->stride; };
+  auto len_of = [&](uint32_t i) { return b->lens ? b->lens[i] : b->fixed_len; };
+
+  // Chunks: runs of consecutive packets whose 16-byte envelope fits kChunk
+  // (a single larger packet forms its own chunk).  Host offsets are kept mod
+  // 16 in staging, so address parity (in_cksum_hdr) is preserved.
+  auto chunk_end = [&](uint32_t i, uint64_t *s0, uint64_t *end) {
+    *s0 = off_of(i) & ~15ull;
+    *end = off_of(i) + len_of(i);
+    uint32_t j = i + 1;
+    while (j < b->n) {
+      const uint64_t o = off_of(j), e = o + len_of(j);
+      if (o < *s0 || e - *s0 > kChunk) break;
+      if (e > *end) *end = e;
+      ++j;
+    }
+    return j;
+  };
+  uint32_t max_pk = 0, max_len = 0;
+  uint64_t need_stage = 0;
+  for (uint32_t i = 0; i < b->n;) {
+    uint64_t s0, end;
+    const uint32_t j = chunk_end(i, &s0, &end);
+    if (j - i > max_pk) max_pk = j - i;
+    if (end - s0 > need_stage) need_stage = end - s0;
+    i = j;
+  }
+  for (uint32_t i = 0; i < b->n; ++i) max_len = len_of(i) > max_len ? len_of(i) : max_len;
+  need_stage = (need_stage + 64) & ~15ull;
+  if (need_stage > kMaxBytes) return set_err(-E2BIG, "packet too large for staging");
+
+  if (!c.hstream[0])
+    for (int k = 0; k < ThreadCtx::kRing; ++k)
+      HIP_TRY(hipStreamCreateWithFlags(&c.hstream[k], hipStreamNonBlocking));
+  if (!c.dbad) HIP_TRY(hipMalloc(&c.dbad, 4 * ThreadCtx::kRing));
+  if (c.dstage_cap < need_stage) {
+    for (int k = 0; k < ThreadCtx::kRing; ++k) {
+      if (c.dstage[k]) HIP_TRY(hipFree(c.dstage[k]));
+      HIP_TRY(hipMalloc(&c.dstage[k], need_stage));
+    }
+    c.dstage_cap = need_stage;
+  }
+  if (c.dout_cap < max_pk) {
+    for (int k = 0; k < ThreadCtx::kRing; ++k) {
+      if (c.dout[k]) HIP_TRY(hipFree(c.dout[k]));
+      if (c.dst8[k]) HIP_TRY(hipFree(c.dst8[k]));
+      if (c.ddesc[k]) HIP_TRY(hipFree(c.ddesc[k]));
+      if (c.hdesc[k]) HIP_TRY(hipHostFree(c.hdesc[k]));
+      HIP_TRY(hipMalloc(&c.dout[k], 4ull * max_pk));
+      HIP_TRY(hipMalloc(&c.dst8[k], (size_t)max_pk + 16));
+      HIP_TRY(hipMalloc(&c.ddesc[k], 12ull * max_pk));
+      HIP_TRY(hipHostMalloc((void **)&c.hdesc[k], 12ull * max_pk, hipHostMallocDefault));
+    }
+    c.dout_cap = max_pk;
+  }
+  HIP_TRY(hipMemsetAsync(c.dbad, 0, 4 * ThreadCtx::kRing, c.hstream[0]));
+  HIP_TRY(hipStreamSynchronize(c.hstream[0]));
+
+  const int G = pick_group(max_len);
+  bool used[ThreadCtx::kRing] = {};
+  int k = 0;
+  for (uint32_t i = 0; i < b->n;) {
+    uint64_t s0, end;
+    const uint32_t j = chunk_end(i, &s0, &end);
+    hipStream_t st = c.hstream[k];
+    Desc d{};
+    d.base = c.dstage[k];
+    d.bytes = (uint32_t)((end - s0 + 15u) & ~15ull);
+    d.n = j - i;
+    if (var) {
+      // rebased descriptors travel with the chunk; the pinned slot is reused
+      // only once the stream has finished its previous copy out of it
+      if (used[k]) HIP_TRY(hipStreamSynchronize(st));
+      uint64_t *ho = (uint64_t *)c.hdesc[k];
+      uint32_t *hl = (uint32_t *)(c.hdesc[k] + 8ull * max_pk);
+      for (uint32_t q = 0; q < d.n; ++q) {
+        ho[q] = off_of(i + q) - s0;
+        hl[q] = len_of(i + q);
+      }
+      HIP_TRY(hipMemcpyAsync(c.ddesc[k], c.hdesc[k], 12ull * max_pk, hipMemcpyHostToDevice, st));
+      d.offs = (const uint64_t *)c.ddesc[k];
+      d.lens = (const uint32_t *)(c.ddesc[k] + 8ull * max_pk);
+    } else {
+      d.first_off = off_of(i) - s0;
+      d.stride = b->stride;
+      d.fixed_len = b->fixed_len;
+    }
+    HIP_TRY(hipMemcpyAsync(c.dstage[k], hb + s0, end - s0, hipMemcpyHostToDevice, st));
+    uint16_t *dip = c.dout[k], *dl4 = c.dout[k] + max_pk;
+    rc = launch_verify(d, G, ip_sum ? dip : nullptr, l4_sum ? dl4 : nullptr,
+                       status ? c.dst8[k] : nullptr, c.dbad + k, st);
+    if (rc) return rc;
+    if (ip_sum) HIP_TRY(hipMemcpyAsync(ip_sum + i, dip, 2ull * d.n, hipMemcpyDeviceToHost, st));
+    if (l4_sum) HIP_TRY(hipMemcpyAsync(l4_sum + i, dl4, 2ull * d.n, hipMemcpyDeviceToHost, st));
+    if (status) HIP_TRY(hipMemcpyAsync(status + i, c.dst8[k], d.n, hipMemcpyDeviceToHost, st));
+    used[k] = true;
+    i = j;
+    k = (k + 1) % ThreadCtx::kRing;
+  }
+  uint32_t bads[ThreadCtx::kRing] = {};
+  for (int q = 0; q < ThreadCtx::kRing; ++q) HIP_TRY(hipStreamSynchronize(c.hstream[q]));
+  HIP_TRY(hipMemcpy(bads, c.dbad, sizeof bads, hipMemcpyDeviceToHost));
+  if (bad_count) {
+    uint32_t t = 0;
+    for (int q = 0; q < ThreadCtx::kRing; ++q) t += bads[q];
+    *bad_count = t;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------- (b1) scalar bridge
+uint8_t *mi__scalar_staging(size_t need) {
+  if (ensure_ctx()) return nullptr;
+  ThreadCtx &c = t_ctx;
+  if (need < 4096) need = 4096;
+  if (c.stage_cap < need) {
+    if (c.stage) (void)hipHostFree(c.stage);
+    c.stage = nullptr;
+    c.stage_cap = 0;
+    size_t cap = 1;
+    while (cap < need) cap <<= 1;
+    hipError_t e = hipHostMalloc((void **)&c.stage, cap, hipHostMallocMapped);
+    if (e != hipSuccess) {
+      set_err(-ENOMEM, "hipHostMalloc(%zu): %s", cap, hipGetErrorString(e));
+      return nullptr;
+    }
+    c.stage_cap = cap;
+  }
+  return c.stage;
+}
+
+int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32_t src,
+                    uint32_t dst, uint8_t proto, uint32_t plen, uint16_t *out) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  ThreadCtx &c = t_ctx;
+  if (!c.stage || off + len > c.stage_cap || c.stage_cap > kMaxBytes)
+    return set_err(-EINVAL, "scalar staging overrun");
+  if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
+  if (!c.sout) HIP_TRY(hipHostMalloc((void **)&c.sout, 64, hipHostMallocMapped));
+  uint8_t *dstage = nullptr;
+  uint16_t *dout = nullptr;
+  HIP_TRY(hipHostGetDevicePointer((void **)&dstage, c.stage, 0));
+  HIP_TRY(hipHostGetDevicePointer((void **)&dout, c.sout, 0));
+  hipLaunchKernelGGL(k_scalar, dim3(1), dim3(64), 0, c.sstream, (const uint8_t *)dstage,
+                     (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u,
+                     pseudo, src, dst, (uint32_t)proto, plen, dout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c.sstream));
+  *out = *(volatile uint16_t *)c.sout;
+  return 0;
+}
+
+void mi__fatal(const char *what) {
+  fprintf(stderr, "libmicksum: %s: %s\n", what, t_err[0] ? t_err : "unknown error");
+  fflush(stderr);
+  abort();
+}
+
+}  // extern "C"

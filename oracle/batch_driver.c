@@ -1,0 +1,239 @@
+/*
+ * oracle/batch_driver.c -- drives the scalar checksum functions over packet
+ * batches the way the reference's protocol code calls them.
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.h).  Compiled twice by oracle/Makefile:
+ *   -DPFX=orc_  against the restatement (cksum_oracle.c)
+ *   -DPFX=ref_  against the reference's own in_cksum.o (symbols renamed ref_*)
+ *
+ * Call patterns restated:
+ *   RX  ip_input.c:459-471   hlen == 20 ? in_cksum_hdr(ip) : in_cksum(m, hlen)
+ *       tcp_input.c:697,714  tlen = ntohs(ip_len) - off0;
+ *                            in_cksum_pseudo_header(m, tlen, off0, src, dst, p)
+ *   TX  ip_output.c:649-654 -> in_delayed_cksum (ip_output.c:958-983):
+ *                            in_cksum_skip(m, ip_len, hl<<2), UDP 0 -> 0xffff,
+ *                            stored at hl + csum_data (TCP 16, UDP 6) if inside m_len
+ *       ip_output.c:667-672  ip_sum = 0; ip_sum = in_cksum(m, hlen)
+ */
+#include <pthread.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "oracle.h"
+
+#define CAT_(a, b) a##b
+#define CAT(a, b) CAT_(a, b)
+#define F(name) CAT(PFX, name)
+
+/* The scalar functions this build drives (orc_* or ref_*). */
+uint16_t F(in_cksum_skip)(struct orc_mbuf *m, int len, int skip);
+uint16_t F(in_cksum_pseudo_header)(struct orc_mbuf *m, int plen, int off0,
+                                   uint32_t src, uint32_t dst, uint8_t protonum);
+unsigned F(in_cksum_hdr)(const void *ip);
+
+/* A full 256-byte mbuf, as the reference allocates (param.h:159 MSIZE). */
+union drv_mbuf {
+	struct orc_mbuf m;
+	char pad[256];
+};
+
+static inline uint64_t pkt_off(const uint64_t *offs, uint64_t stride,
+                               uint64_t first_off, uint32_t i)
+{
+	return offs ? offs[i] : first_off + (uint64_t)i * stride;
+}
+
+static inline uint32_t ld32(const uint8_t *p)
+{
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return v;
+}
+
+struct job {
+	const uint8_t *base;
+	uint8_t *wbase;
+	const uint64_t *offs;
+	uint64_t stride, first_off;
+	const uint32_t *flen;
+	uint32_t fixed_flen, lo, hi;
+	uint16_t *ip_out, *l4_out;
+	uint8_t *status;
+};
+
+static void verify_range(const struct job *j)
+{
+	for (uint32_t i = j->lo; i < j->hi; i++) {
+		const uint8_t *ip = j->base + pkt_off(j->offs, j->stride, j->first_off, i);
+		uint32_t fl = j->flen ? j->flen[i] : j->fixed_flen;
+		uint16_t ipsum = 0, l4 = 0;
+		uint8_t st = 0;
+		union drv_mbuf mb;
+		memset(&mb, 0, sizeof(mb));
+		mb.m.m_data = (char *)ip;
+		mb.m.m_len = (int32_t)fl;
+		if (fl < 20) {
+			st = ORC_ST_MALFORMED;
+		} else {
+			uint32_t hl = (uint32_t)(ip[0] & 0x0f) << 2;
+			uint32_t iplen = ((uint32_t)ip[2] << 8) | ip[3];
+			if (hl < 20 || hl > fl) {
+				st = ORC_ST_MALFORMED;
+			} else {
+				ipsum = (hl == 20) ? (uint16_t)F(in_cksum_hdr)(ip)
+				                   : F(in_cksum_skip)(&mb.m, (int)hl, 0);
+				if (iplen < hl || iplen > fl)
+					st |= ORC_ST_MALFORMED;
+				else
+					l4 = F(in_cksum_pseudo_header)(&mb.m, (int)(iplen - hl),
+					    (int)hl, ld32(ip + 12), ld32(ip + 16), ip[9]);
+				if (ipsum)
+					st |= ORC_ST_IP_BAD;
+				if (l4)
+					st |= ORC_ST_L4_BAD;
+			}
+		}
+		if (j->ip_out)
+			j->ip_out[i] = ipsum;
+		if (j->l4_out)
+			j->l4_out[i] = l4;
+		if (j->status)
+			j->status[i] = st;
+	}
+}
+
+static void finalize_range(const struct job *j)
+{
+	for (uint32_t i = j->lo; i < j->hi; i++) {
+		uint8_t *ip = j->wbase + pkt_off(j->offs, j->stride, j->first_off, i);
+		uint32_t fl = j->flen ? j->flen[i] : j->fixed_flen;
+		uint32_t hl, iplen;
+		union drv_mbuf mb;
+		if (fl < 20)
+			continue;
+		hl = (uint32_t)(ip[0] & 0x0f) << 2;
+		iplen = ((uint32_t)ip[2] << 8) | ip[3];
+		if (hl < 20 || hl > fl || iplen < hl || iplen > fl)
+			continue;
+		memset(&mb, 0, sizeof(mb));
+		mb.m.m_data = (char *)ip;
+		mb.m.m_len = (int32_t)fl;
+		if (ip[9] == 6 || ip[9] == 17) {
+			uint16_t c = F(in_cksum_skip)(&mb.m, (int)iplen, (int)hl);
+			uint32_t at = hl + (ip[9] == 6 ? 16u : 6u);
+			if (ip[9] == 17 && c == 0)
+				c = 0xffff;
+			if (at + 2 <= fl)
+				memcpy(ip + at, &c, 2);
+		}
+		ip[10] = ip[11] = 0;
+		{
+			uint16_t c = F(in_cksum_skip)(&mb.m, (int)hl, 0);
+			memcpy(ip + 10, &c, 2);
+		}
+	}
+}
+
+static void *verify_thr(void *a) { verify_range((const struct job *)a); return NULL; }
+static void *finalize_thr(void *a) { finalize_range((const struct job *)a); return NULL; }
+
+static void run_jobs(struct job *proto, uint32_t n, int nthreads, void *(*fn)(void *))
+{
+	enum { MAXT = 256 };
+	pthread_t th[MAXT];
+	struct job jobs[MAXT];
+	int t, started = 0;
+	if (nthreads < 1)
+		nthreads = 1;
+	if (nthreads > MAXT)
+		nthreads = MAXT;
+	if ((uint32_t)nthreads > n)
+		nthreads = n ? (int)n : 1;
+	for (t = 0; t < nthreads; t++) {
+		jobs[t] = *proto;
+		jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+		jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+	}
+	if (nthreads == 1) {
+		fn(&jobs[0]);
+		return;
+	}
+	for (t = 1; t < nthreads; t++)
+		if (pthread_create(&th[t], NULL, fn, &jobs[t]) == 0)
+			started = t;
+		else
+			break;
+	fn(&jobs[0]);
+	for (t = started + 1; t < nthreads; t++) /* threads that failed to start */
+		fn(&jobs[t]);
+	for (t = 1; t <= started; t++)
+		pthread_join(th[t], NULL);
+}
+
+void F(ipv4_verify_batch)(const uint8_t *base, const uint64_t *offs,
+    uint64_t stride, uint64_t first_off, const uint32_t *flen,
+    uint32_t fixed_flen, uint32_t n, uint16_t *ip_out, uint16_t *l4_out,
+    uint8_t *status, int nthreads)
+{
+	struct job j = { base, NULL, offs, stride, first_off, flen, fixed_flen,
+	                 0, n, ip_out, l4_out, status };
+	run_jobs(&j, n, nthreads, verify_thr);
+}
+
+void F(ipv4_finalize_batch)(uint8_t *base, const uint64_t *offs,
+    uint64_t stride, uint64_t first_off, const uint32_t *flen,
+    uint32_t fixed_flen, uint32_t n, int nthreads)
+{
+	struct job j = { base, base, offs, stride, first_off, flen, fixed_flen,
+	                 0, n, NULL, NULL, NULL };
+	run_jobs(&j, n, nthreads, finalize_thr);
+}
+
+/* One span, in_cksum_skip(m, len, 0) repeated: the 64 KiB plumbing config. */
+uint64_t F(skip_repeat)(const uint8_t *buf, int len, int iters)
+{
+	union drv_mbuf mb;
+	uint64_t acc = 0;
+	memset(&mb, 0, sizeof(mb));
+	mb.m.m_data = (char *)buf;
+	mb.m.m_len = len;
+	for (int k = 0; k < iters; k++)
+		acc += F(in_cksum_skip)(&mb.m, len, 0);
+	return acc;
+}
+
+/* Build an mbuf chain over caller segments (seglen may be 0). */
+static void build_chain(union drv_mbuf *mb, const uint8_t *const *seg,
+                        const int32_t *seglen, int nseg)
+{
+	for (int k = 0; k < nseg; k++) {
+		memset(&mb[k], 0, sizeof(mb[k]));
+		mb[k].m.m_data = (char *)seg[k];
+		mb[k].m.m_len = seglen[k];
+		mb[k].m.m_next = (k + 1 < nseg) ? &mb[k + 1].m : NULL;
+	}
+}
+
+#define MAX_SEGS 64
+
+uint16_t F(chain_skip)(const uint8_t *const *seg, const int32_t *seglen,
+                       int nseg, int len, int skip)
+{
+	union drv_mbuf mb[MAX_SEGS];
+	if (nseg < 1 || nseg > MAX_SEGS)
+		return 0;
+	build_chain(mb, seg, seglen, nseg);
+	return F(in_cksum_skip)(&mb[0].m, len, skip);
+}
+
+uint16_t F(chain_pseudo)(const uint8_t *const *seg, const int32_t *seglen,
+                         int nseg, int plen, int off0, uint32_t src,
+                         uint32_t dst, uint8_t proto)
+{
+	union drv_mbuf mb[MAX_SEGS];
+	if (nseg < 1 || nseg > MAX_SEGS)
+		return 0;
+	build_chain(mb, seg, seglen, nseg);
+	return F(in_cksum_pseudo_header)(&mb[0].m, plen, off0, src, dst, proto);
+}

@@ -1,0 +1,150 @@
+"""ctypes front-end for the CPU checker libraries.
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, ``__graft_entry__.smoke()`` and
+bench.py's ``cpu_baseline`` leg -- never by the product (``libunsod_amd``).
+
+Two implementations share one interface:
+
+* ``Oracle("port")``      -- oracle/_build/liboracle.so, the from-scratch C
+  restatement of src/sys/amd64/amd64/in_cksum.c (cksum_oracle.c);
+* ``Oracle("reference")`` -- oracle/_ref/libref.so, the reference's own
+  in_cksum.c compiled from /root/reference by oracle/Makefile (symbols renamed
+  ``ref_*``).  Built in the dev container; the prebuilt .so travels to the GPU
+  box, the reference tree does not.
+
+Mbuf chains are built in C (batch_driver.c) over caller segments, so a segment's
+*address* is real: ``place()`` puts bytes at a chosen address mod 64, which is
+what ``in_cksum_hdr``'s absolute-address lanes and the chain-walk parity swap
+(in_cksum.c:222-225) depend on.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATHS = {
+    "port": os.path.join(_HERE, "_build", "liboracle.so"),
+    "reference": os.path.join(_HERE, "_ref", "libref.so"),
+}
+_PFX = {"port": "orc_", "reference": "ref_"}
+
+u8p = C.POINTER(C.c_uint8)
+u16p = C.POINTER(C.c_uint16)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+
+
+def available(kind: str) -> bool:
+    return os.path.exists(LIB_PATHS[kind])
+
+
+def place(data, addr_mod: int, align: int = 64, pad: int = 64) -> tuple[np.ndarray, int]:
+    """Copy ``data`` into a fresh buffer so that its first byte sits at an
+    address == addr_mod (mod align).  Returns (keepalive_array, address).
+    ``pad`` slack bytes surround it (in_cksumdata reads up to 3 B either side)."""
+    src = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    n = int(src.size)
+    buf = np.zeros(n + 2 * pad + 2 * align, dtype=np.uint8)
+    base = buf.ctypes.data
+    start = pad + ((addr_mod - (base + pad)) % align)
+    buf[start:start + n] = src
+    return buf, base + start
+
+
+def _ptr(a: np.ndarray | None, typ):
+    return None if a is None else a.ctypes.data_as(typ)
+
+
+class Oracle:
+    def __init__(self, kind: str = "port"):
+        if kind not in LIB_PATHS:
+            raise ValueError(kind)
+        path = LIB_PATHS[kind]
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        self.kind = kind
+        self.lib = C.CDLL(path)
+        p = _PFX[kind]
+        g = lambda n: getattr(self.lib, p + n)  # noqa: E731
+
+        self._skip = g("in_cksum_skip")
+        self._hdr = g("in_cksum_hdr"); self._hdr.restype = C.c_uint; self._hdr.argtypes = [C.c_void_p]
+        self._pseudo = g("in_pseudo"); self._pseudo.restype = C.c_uint16
+        self._pseudo.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32]
+        self._addword = g("in_addword"); self._addword.restype = C.c_uint16
+        self._addword.argtypes = [C.c_uint16, C.c_uint16]
+
+        self._chain_skip = g("chain_skip"); self._chain_skip.restype = C.c_uint16
+        self._chain_skip.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.c_int, C.c_int, C.c_int]
+        self._chain_pseudo = g("chain_pseudo"); self._chain_pseudo.restype = C.c_uint16
+        self._chain_pseudo.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_int32), C.c_int, C.c_int,
+                                       C.c_int, C.c_uint32, C.c_uint32, C.c_uint8]
+        self._verify = g("ipv4_verify_batch"); self._verify.restype = None
+        self._verify.argtypes = [C.c_void_p, u64p, C.c_uint64, C.c_uint64, u32p, C.c_uint32,
+                                 C.c_uint32, u16p, u16p, u8p, C.c_int]
+        self._final = g("ipv4_finalize_batch"); self._final.restype = None
+        self._final.argtypes = [C.c_void_p, u64p, C.c_uint64, C.c_uint64, u32p, C.c_uint32,
+                                C.c_uint32, C.c_int]
+        self._repeat = g("skip_repeat"); self._repeat.restype = C.c_uint64
+        self._repeat.argtypes = [C.c_void_p, C.c_int, C.c_int]
+
+    # --- scalar reference entry points (in_cksum.h:77-83) -------------------
+    def in_pseudo(self, a: int, b: int, c: int) -> int:
+        return int(self._pseudo(a & 0xFFFFFFFF, b & 0xFFFFFFFF, c & 0xFFFFFFFF))
+
+    def in_addword(self, a: int, b: int) -> int:
+        return int(self._addword(a & 0xFFFF, b & 0xFFFF))
+
+    def in_cksum_hdr_at(self, addr: int) -> int:
+        return int(self._hdr(C.c_void_p(addr)))
+
+    def in_cksum_hdr(self, data20, addr_mod: int = 0) -> int:
+        keep, addr = place(data20, addr_mod)
+        r = self.in_cksum_hdr_at(addr)
+        del keep
+        return r
+
+    @staticmethod
+    def _segs(segs: Sequence[tuple[bytes, int]]):
+        keep, addrs, lens = [], [], []
+        for data, mod in segs:
+            k, a = place(data, mod)
+            keep.append(k); addrs.append(a); lens.append(len(data))
+        n = len(segs)
+        return keep, (C.c_void_p * n)(*addrs), (C.c_int32 * n)(*lens), n
+
+    def chain_skip(self, segs: Sequence[tuple[bytes, int]], length: int, skip: int) -> int:
+        keep, a, l, n = self._segs(segs)
+        r = int(self._chain_skip(a, l, n, length, skip))
+        del keep
+        return r
+
+    def chain_pseudo(self, segs, plen: int, off0: int, src: int, dst: int, proto: int) -> int:
+        keep, a, l, n = self._segs(segs)
+        r = int(self._chain_pseudo(a, l, n, plen, off0, src & 0xFFFFFFFF, dst & 0xFFFFFFFF, proto & 0xFF))
+        del keep
+        return r
+
+    # --- batch drivers ------------------------------------------------------
+    def ipv4_verify_batch(self, buf: np.ndarray, n: int, *, offs=None, stride: int = 0,
+                          first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1):
+        ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
+        offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
+        flen = None if flen is None else np.ascontiguousarray(flen, np.uint32)
+        self._verify(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
+                     fixed_flen, n, _ptr(ip, u16p), _ptr(l4, u16p), _ptr(st, u8p), nthreads)
+        return ip, l4, st
+
+    def ipv4_finalize_batch(self, buf: np.ndarray, n: int, *, offs=None, stride: int = 0,
+                            first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1):
+        offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
+        flen = None if flen is None else np.ascontiguousarray(flen, np.uint32)
+        self._final(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
+                    fixed_flen, n, nthreads)
+
+    def skip_repeat(self, buf: np.ndarray, length: int, iters: int) -> int:
+        return int(self._repeat(buf.ctypes.data, length, iters))

@@ -1,0 +1,53 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden", "cksum_golden.npz")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libmicksum's HIP kernels)")
+
+
+def pytest_collection_modifyitems(config, items):
+    try:
+        import torch
+        have_gpu = torch.cuda.is_available()
+    except Exception:  # pragma: no cover
+        have_gpu = False
+    if have_gpu:
+        return
+    skip = pytest.mark.skip(reason="no GPU in this environment (gpu tests run on the MI355X box)")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def chain_segments(g, seg0: int, nseg: int):
+    """[(bytes, addr_mod)] of a golden chain."""
+    out = []
+    for s in range(seg0, seg0 + nseg):
+        off, ln, mod = int(g["seg_off"][s]), int(g["seg_len"][s]), int(g["seg_mod"][s])
+        out.append((g["blob"][off:off + ln].tobytes(), mod))
+    return out
+
+
+def aligned(a: np.ndarray, align: int = 64):
+    """Copy of ``a`` at an address == 0 (mod align); returns (keepalive, view)."""
+    raw = np.zeros(a.size + 2 * align, np.uint8)
+    s = (-raw.ctypes.data) % align
+    v = raw[s:s + a.size]
+    v[:] = a
+    return raw, v

@@ -1,0 +1,241 @@
+"""Parity of the HIP path against the oracle and the reference's golden vectors.
+
+Every comparison is bit-exact (integer work).  All calls go through
+libmicksum.so's C ABI: the drop-in in_cksum* symbols over real mbuf chains, and
+the batch kernels over device tensors.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import aligned, chain_segments
+from oracle.pyoracle import Oracle
+
+import libunsod_amd as mi
+from libunsod_amd import synth
+
+pytestmark = pytest.mark.gpu
+ORC = Oracle("port")
+
+
+def dev_tensor(a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def cpu(t):
+    return t.cpu().numpy()
+
+
+# ------------------------------------------------- (b1) drop-ins vs golden
+def test_dropin_skip_golden(golden):
+    g = golden
+    bad = []
+    for k in range(len(g["sk_result"])):
+        segs = chain_segments(g, int(g["sk_seg0"][k]), int(g["sk_nseg"][k]))
+        r = mi.in_cksum_skip(mi.MbufChain(segs), int(g["sk_len"][k]), int(g["sk_skip"][k]))
+        if r != int(g["sk_result"][k]):
+            bad.append(k)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+def test_dropin_pseudo_golden(golden):
+    g = golden
+    bad = []
+    for k in range(len(g["ps_result"])):
+        segs = chain_segments(g, int(g["ps_seg0"][k]), int(g["ps_nseg"][k]))
+        r = mi.in_cksum_pseudo_header(mi.MbufChain(segs), int(g["ps_plen"][k]), int(g["ps_off0"][k]),
+                                      int(g["ps_src"][k]), int(g["ps_dst"][k]), int(g["ps_proto"][k]))
+        if r != int(g["ps_result"][k]):
+            bad.append(k)
+    assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
+
+
+def test_dropin_hdr_golden(golden):
+    g = golden
+    for k in range(len(g["hd_result"])):
+        off = int(g["hd_off"][k])
+        assert mi.in_cksum_hdr(g["blob"][off:off + 20].tobytes(), int(g["hd_mod"][k])) == int(g["hd_result"][k])
+
+
+# -------------------------------------------------- (b2) batch vs golden
+def test_verify_golden(golden):
+    g = golden
+    n = len(g["vb_offs"])
+    buf = dev_tensor(g["ver_in"])
+    b = mi.PktBatch(buf, n, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                    lens=dev_tensor(g["vb_flen"].astype(np.int32)))
+    r = mi.ipv4_verify(b, bad_count=True)
+    assert np.array_equal(cpu(r["ip"]), g["ver_ip"])
+    assert np.array_equal(cpu(r["l4"]), g["ver_l4"])
+    assert np.array_equal(cpu(r["status"]), g["ver_st"])
+    assert int(r["bad"].item()) == int((g["ver_st"] != 0).sum())
+
+
+def test_finalize_golden(golden):
+    g = golden
+    n = len(g["vb_offs"])
+    buf = dev_tensor(g["fin_in"])
+    b = mi.PktBatch(buf, n, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                    lens=dev_tensor(g["vb_flen"].astype(np.int32)))
+    mi.ipv4_finalize(b)
+    assert np.array_equal(cpu(buf), g["fin_out"])
+    sl = dev_tensor(g["slot_in"])
+    mi.ipv4_finalize(mi.PktBatch(sl, 64, stride=2176, first_off=142, fixed_len=1500))
+    assert np.array_equal(cpu(sl), g["slot_out"])
+
+
+# ------------------------------------------------------- spans vs oracle
+@pytest.mark.parametrize("max_len", [0, 64, 300, 1500, 9100, 70000])
+def test_span_batch_random(max_len):
+    rng = np.random.default_rng(max_len + 5)
+    n = 400
+    hi = max(max_len, 64) if max_len else 2000
+    lens = rng.integers(0, hi + 1, n)
+    lens[:5] = [0, 1, 2, 3, hi]
+    offs = synth.packed_offsets(lens, first_off=int(rng.integers(0, 16)), align=1) + \
+        np.arange(n, dtype=np.uint64) * 3  # every alignment / parity
+    size = int(offs[-1] + lens[-1]) + 64
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    host[int(offs[7]):int(offs[7] + lens[7])] = 0       # all-zero span
+    host[int(offs[8]):int(offs[8] + lens[8])] = 0xFF    # all-ones span
+    buf = dev_tensor(host)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)),
+                    max_len=max_len)
+    _, h = aligned(host)
+    seeds = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    proto = rng.integers(0, 256, n).astype(np.uint8)
+    plens = (lens + rng.integers(0, 3, n) * 65536).astype(np.uint32)  # plen truncates to 16 bits in the seed
+
+    got_skip = cpu(mi.span_batch(b))
+    got_abs = cpu(mi.span_batch(b, mi.MI_SPAN_ABS))
+    got_ps = cpu(mi.span_batch(b, src=dev_tensor(src), dst=dev_tensor(dst), proto=dev_tensor(proto),
+                               plens=dev_tensor(plens)))
+    got_seed = cpu(mi.span_batch(b, seeds=dev_tensor(seeds)))
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        seg = h[o:o + L].tobytes()
+        want = ORC.chain_skip([(seg, o % 64)], L, 0)
+        assert got_skip[i] == want, (i, L, o)
+        # absolute lanes: byte-swapped at odd addresses (in_cksum.c:278-285)
+        wa = want if o % 2 == 0 else ((want & 0xFF) << 8) | (want >> 8)
+        assert got_abs[i] == wa, (i, L, o)
+        # pseudo-header: a one-mbuf chain with the span at off0 = 0; plen beyond the
+        # chain truncates the walk silently but still seeds (uint16_t)plen
+        wp = ORC.chain_pseudo([(seg, o % 64)], int(plens[i]), 0, int(src[i]), int(dst[i]), int(proto[i]))
+        assert got_ps[i] == wp, (i, L)
+        # explicit seed == complement of fold(seed + S)
+        s = (~want & 0xFFFF) + int(seeds[i])
+        f = 0 if s == 0 else 1 + (s - 1) % 65535
+        assert got_seed[i] == (~f & 0xFFFF)
+
+
+def test_span_pseudo_plen_truncation():
+    """in_cksum_pseudo_header uses (uint16_t)plen in the seed (in_cksum.c:252-253)."""
+    rng = np.random.default_rng(3)
+    for L in (65515, 65536, 65536 + 20):
+        data = rng.integers(0, 256, L, dtype=np.uint8)
+        buf = dev_tensor(np.concatenate([data, np.zeros(64, np.uint8)]))
+        b = mi.PktBatch(buf, 1, first_off=0, stride=0, fixed_len=L)
+        src = np.array([0x0101A8C0], np.uint32); dst = np.array([0x0201A8C0], np.uint32); pr = np.array([6], np.uint8)
+        got = cpu(mi.span_batch(b, src=dev_tensor(src), dst=dev_tensor(dst), proto=dev_tensor(pr)))[0]
+        want = ORC.chain_pseudo([(data.tobytes(), 0)], L, 0, int(src[0]), int(dst[0]), 6)
+        assert got == want
+
+
+# --------------------------------------------- full-size configs (properties)
+CONFIGS = {
+    "1500": dict(n=65536, L=1500, stride=synth.STRIDE_1500, first=synth.IP_OFF),
+    "9000": dict(n=65536, L=9000, stride=synth.STRIDE_9000, first=synth.IP_OFF),
+    "64": dict(n=1 << 20, L=synth.MIN_FRAME_IP_LEN, stride=synth.STRIDE_64, first=synth.ETH_HLEN),
+}
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_full_size_config(name):
+    """BASELINE configs at full size: device-generated batch -> TX finalize ->
+    RX verify must be all-valid; 1 % corrupted packets must be exactly the ones
+    flagged; finalize output and verify outputs are compared bit-for-bit with the
+    oracle over the whole batch."""
+    c = CONFIGS[name]
+    n, L, stride, first = c["n"], c["L"], c["stride"], c["first"]
+    size = first + (n - 1) * stride + L + 64
+    buf = torch.empty(size, dtype=torch.uint8, device="cuda")
+    b = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
+    mi.synth_ipv4(b, seed=0x5EED5EED)
+    raw = cpu(buf).copy()
+    mi.ipv4_finalize(b)
+    fin = cpu(buf)
+    _, ref = aligned(raw)
+    ORC.ipv4_finalize_batch(ref, n, stride=stride, first_off=first, fixed_flen=L, nthreads=8)
+    assert np.array_equal(fin, ref)
+    r = mi.ipv4_verify(b, bad_count=True)
+    assert int(r["bad"].item()) == 0
+    assert not cpu(r["ip"]).any() and not cpu(r["l4"]).any() and not cpu(r["status"]).any()
+    # corrupt 1 %
+    rng = np.random.default_rng(11)
+    bad = np.sort(rng.choice(n, n // 100, replace=False))
+    pos = first + bad.astype(np.int64) * stride + rng.integers(0, L, bad.size)
+    flip = (1 << rng.integers(0, 8, bad.size)).astype(np.uint8)
+    fin[pos] ^= flip
+    buf.copy_(torch.from_numpy(fin))
+    r = mi.ipv4_verify(b, bad_count=True)
+    st = cpu(r["status"])
+    assert np.array_equal(np.nonzero(st)[0], bad)
+    assert int(r["bad"].item()) == bad.size
+    ip, l4, st_o = ORC.ipv4_verify_batch(fin, n, stride=stride, first_off=first, fixed_flen=L, nthreads=8)
+    assert np.array_equal(cpu(r["ip"]), ip) and np.array_equal(cpu(r["l4"]), l4)
+    assert np.array_equal(st, st_o)
+
+
+def test_pareto_mixed():
+    """Mixed 64-9000 B (Pareto) batch packed at 8-byte offsets."""
+    n = 1 << 16
+    lens = synth.pareto_lengths(n)
+    offs = synth.packed_offsets(lens, first_off=2)
+    b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), payload="pattern")
+    host = b0["buf"]
+    _, ref = aligned(host)
+    ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32), nthreads=8)
+    buf = dev_tensor(host)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)))
+    mi.ipv4_finalize(b)
+    assert np.array_equal(cpu(buf), ref)
+    r = mi.ipv4_verify(b)
+    assert not cpu(r["status"]).any()
+
+
+def test_host_path_matches_device():
+    n, L, stride, first = 4096, 1500, 2176, 142
+    b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=5)
+    host = b0["buf"]
+    ORC.ipv4_finalize_batch(host, n, stride=stride, first_off=first, fixed_flen=L)
+    host[first + 5 * stride + 100] ^= 1
+    ip, l4, st, bad = mi.ipv4_verify_host(host, n, stride=stride, first_off=first, fixed_len=L)
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(host, n, stride=stride, first_off=first, fixed_flen=L)
+    assert np.array_equal(ip, ip_o) and np.array_equal(l4, l4_o) and np.array_equal(st, st_o) and bad == 1
+    # variable layout through the host path
+    lens = synth.pareto_lengths(3000, seed=9)
+    offs = synth.packed_offsets(lens, first_off=6)
+    b1 = synth.build_ipv4_batch(3000, lens, offs=offs.astype(np.int64), seed=6)
+    h1 = b1["buf"]
+    ORC.ipv4_finalize_batch(h1, 3000, offs=offs, flen=lens.astype(np.uint32))
+    ip, l4, st, bad = mi.ipv4_verify_host(h1, 3000, offs=offs, lens=lens)
+    assert bad == 0 and not st.any()
+
+
+def test_deterministic_and_stream_async():
+    n, L = 8192, 1500
+    buf = torch.empty(142 + n * 2176 + 64, dtype=torch.uint8, device="cuda")
+    b = mi.PktBatch(buf, n, stride=2176, first_off=142, fixed_len=L)
+    mi.synth_ipv4(b, seed=1)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        mi.ipv4_finalize(b)
+        r1 = mi.ipv4_verify(b)
+        r2 = mi.ipv4_verify(b)
+    s.synchronize()
+    for k in ("ip", "l4", "status"):
+        assert np.array_equal(cpu(r1[k]), cpu(r2[k]))
+    assert not cpu(r1["status"]).any()
