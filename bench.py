@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled (0: enough for >= 1 GiB)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--streams", type=int, default=1, help="streams the steps alternate over")
     return ap.parse_args()
 
 
@@ -99,7 +100,7 @@ def main():
         cfg = dict(workload=workload, packets_per_gpu=n, ip_datagram_len=L, slot_stride=stride, ip_offset=first)
     size = (size + 255) & ~255
     R = args.rotate or max(1, -(-(1 << 30) // size))  # footprint >= 1 GiB: defeat the 256 MiB MALL
-    cfg.update(rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
+    cfg.update(streams=args.streams, rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
                parallelism=f"dp{world} (independent packet shards, no collective)")
 
     batches, outs = [], []
@@ -123,29 +124,26 @@ def main():
     if int(chk["bad"].item()) != 0:
         raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
 
-    stream = torch.cuda.current_stream()
-    for k in range(args.warmup):
-        mi.ipv4_verify(batches[k % R], out=outs[k % R], stream=stream)
+    nst = max(1, args.streams)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nst - 1)]
+    mi.ipv4_verify_repeat(batches, outs, args.warmup, streams=streams, timing=False)
     torch.cuda.synchronize()
 
     # ------------------------------------------------------- timed region
+    # the K launches are issued back to back from native code (libmicksum), each
+    # bracketed by hipEvents on the stream it runs on
     K = args.steps
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(K):
-        ev0[k].record(stream)
-        mi.ipv4_verify(batches[k % R], out=outs[k % R], stream=stream)
-        ev1[k].record(stream)
+    kern_us = mi.ipv4_verify_repeat(batches, outs, K, streams=streams, timing=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
     elapsed = t1 - t0
-    kern_ms = [ev0[k].elapsed_time(ev1[k]) for k in range(K)]
+    kern_ms = list(kern_us / 1e3)
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

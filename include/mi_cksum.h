@@ -151,6 +151,19 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
                          uint8_t *status, uint32_t *bad_count, void *stream);
 
 /*
+ * Back-to-back submission (the RX burst loop, and the bench): launch `steps`
+ * verify passes, pass k over batch b[k % nb] with outputs ip/l4/status[k % nb]
+ * (arrays of nb device pointers; any array may be NULL), on
+ * streams[k % nstreams] (nstreams = 0: the default stream).  If kernel_us is
+ * non-NULL each pass is bracketed by hipEvents on its own stream and
+ * kernel_us[k] gets its duration.  Synchronous: returns once every pass has
+ * finished.  nb <= 16.
+ */
+int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
+                                uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
+                                void *const *streams, uint32_t nstreams, float *kernel_us);
+
+/*
  * TX finalize in place (ip_output.c:649-672 + in_delayed_cksum :958-983):
  * for TCP/UDP c = in_cksum_skip(m, ip_len, hl) over the pre-seeded L4 header
  * (UDP: 0 -> 0xffff) stored at hl + (TCP 16 | UDP 6) when inside lens[i]; then

@@ -65,6 +65,9 @@ SIGNATURES = {
     "mi_cksum_ipv4_verify": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
     "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
+    "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),
+                                              C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
+                                              C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_float)]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),
@@ -84,6 +87,13 @@ def load() -> C.CDLL:
         raise ImportError(
             f"{LIB_PATH} is missing: the HIP extension must be built "
             "(python -c 'import __graft_entry__ as g; g.build()' or make -C libunsod_amd/csrc)")
+    # torch bundles its own libamdhip64 (SONAME libamdhip64.so.7, NEEDED by torch
+    # as "libamdhip64.so"): load it first so libmicksum binds to that same
+    # runtime instead of pulling a second HIP runtime into the process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)

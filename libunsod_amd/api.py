@@ -172,6 +172,25 @@ def span_batch(b: PktBatch, lanes: int = MI_SPAN_STREAM, *, seeds=None, src=None
     return out
 
 
+def ipv4_verify_repeat(batches, outs, steps: int, streams=None, timing: bool = True):
+    """Launch ``steps`` verify passes back to back from native code (pass k over
+    batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on
+    streams[k % len(streams)] or the current stream).  Synchronous; returns the
+    per-pass kernel durations in microseconds (hipEvents) or None."""
+    nb = len(batches)
+    arr = (PktBatchC * nb)(*[b.c for b in batches])
+    VP = C.c_void_p * nb
+    ptrs = {k: VP(*[_ptr(o.get(k)) for o in outs]) for k in ("ip", "l4", "status")}
+    if streams is None:
+        streams = [None]
+    sh = (C.c_void_p * len(streams))(*[_stream(x) for x in streams])
+    us = (C.c_float * steps)() if timing else None
+    check("mi_cksum_ipv4_verify_repeat",
+          load().mi_cksum_ipv4_verify_repeat(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], steps, sh,
+                                             len(streams), us))
+    return None if us is None else np.frombuffer(us, dtype=np.float32).copy()
+
+
 def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
     """Device-side workload generator (not part of the reference API)."""
     check("mi_cksum_synth_ipv4", load().mi_cksum_synth_ipv4(C.byref(b.c), seed, C.c_void_p(_stream(stream))))
@@ -218,6 +237,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "host_register", "host_unregister", "init", "device_count", "version",
+    "ipv4_verify_host", "ipv4_verify_repeat", "host_register", "host_unregister", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS",
 ]

@@ -66,25 +66,25 @@ __device__ __forceinline__ uint32_t fold16_64(uint64_t s) {
 __device__ __forceinline__ uint32_t swap16(uint32_t x) {
   return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
 }
-// Mask of the bytes [lo, hi) (relative to a 16-byte chunk) inside dword k.
-__device__ __forceinline__ uint32_t dmask(int lo, int hi, int k) {
-  const int a = min(max(lo - 4 * k, 0), 4);
-  const int b = min(max(hi - 4 * k, 0), 4);
-  const uint32_t mb = b >= 4 ? 0xffffffffu : ((1u << (8 * b)) - 1u);
-  const uint32_t ma = a >= 4 ? 0xffffffffu : ((1u << (8 * a)) - 1u);
-  return mb & ~ma;
-}
+// A dword's two 16-bit lanes, added: the absolute-address lanes of in_cksumdata.
 __device__ __forceinline__ uint32_t halves(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
-
-// Sum of the bytes of chunk v that fall in [r0, r1) relative to the packet
-// start, where the chunk starts at `rel` relative to the packet start.
-__device__ __forceinline__ uint32_t chunk_range_sum(const u32x4 &v, int rel, int r0, int r1) {
-  const int lo = min(max(r0 - rel, 0), 16);
-  const int hi = min(max(r1 - rel, 0), 16);
-  if (lo >= hi) return 0u;
-  if (lo == 0 && hi == 16) return halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
-  return halves(v.x & dmask(lo, hi, 0)) + halves(v.y & dmask(lo, hi, 1)) +
-         halves(v.z & dmask(lo, hi, 2)) + halves(v.w & dmask(lo, hi, 3));
+__device__ __forceinline__ uint32_t sum4(const u32x4 &v) {
+  return halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+}
+// Bytes [a, b) of dword w, 0 <= a, b <= 4 (64-bit shifts: a shift by 32 is legal).
+__device__ __forceinline__ uint32_t keep(uint32_t w, int a, int b) {
+  return w & (uint32_t)((~0ull << (8 * a)) & ~(~0ull << (8 * b)));
+}
+// Slow path for chunks that straddle a boundary: the bytes of chunk v (which
+// starts `rel` bytes after the packet start) that lie in [r0, r1) of the packet.
+__device__ __forceinline__ uint32_t range_sum(const u32x4 &v, int rel, int r0, int r1) {
+  const int lo = r0 - rel, hi = r1 - rel;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    s += halves(keep(w[k], min(max(lo - 4 * k, 0), 4), min(max(hi - 4 * k, 0), 4)));
+  return s;
 }
 
 template <int G>
@@ -94,13 +94,13 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
   return x;
 }
 
-// Value of lane k (0..2) of this lane's group.
+// x as held by lane k of this lane's group (k group-uniform).
 template <int G>
-__device__ __forceinline__ uint32_t group_bcast(uint32_t x, int k) {
+__device__ __forceinline__ uint32_t group_lane(uint32_t x, uint32_t k) {
   if constexpr (G == 64) {
-    return __builtin_amdgcn_readlane(x, k);
+    return __builtin_amdgcn_readlane(x, __builtin_amdgcn_readfirstlane(k));
   } else {
-    return __shfl(x, (int)(threadIdx.x & 63u & ~(unsigned)(G - 1)) + k, 64);
+    return __shfl(x, (int)((threadIdx.x & 63u & ~(unsigned)(G - 1)) + k), 64);
   }
 }
 
@@ -130,8 +130,8 @@ __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
-// Issue the kU loads of pass p for a packet whose envelope starts at chunk c0
-// and has nch chunks.
+// Issue the kU loads of pass p for a packet whose envelope starts at byte c0
+// and has nch chunks; chunks past the envelope get the out-of-range offset.
 template <int G>
 __device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0, uint32_t nch,
                                            uint32_t p, int lane, u32x4 (&v)[kU]) {
@@ -142,26 +142,22 @@ __device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0
   }
 }
 
-// Header fields of an IPv4 datagram starting h bytes into chunk 0, read from
-// chunks 0..2 held by lanes 0..2 of the group (pass 0, u = 0).
+// Header fields of an IPv4 datagram that starts h bytes into the envelope,
+// read from the chunks lanes 0..2 of the group hold (pass 0, u = 0): six
+// group-lane reads of the dwords that cover bytes h .. h+23.
 struct IpHdr {
   uint32_t hl, iplen, proto, src, dst;
 };
 template <int G>
 __device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
-  uint32_t D[12];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    D[4 * c + 0] = group_bcast<G>(v0.x, c);
-    D[4 * c + 1] = group_bcast<G>(v0.y, c);
-    D[4 * c + 2] = group_bcast<G>(v0.z, c);
-    D[4 * c + 3] = group_bcast<G>(v0.w, c);
-  }
   const uint32_t q = h >> 2, rb = h & 3u;
   uint32_t T[6];
 #pragma unroll
-  for (int j = 0; j < 6; ++j)
-    T[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
+  for (int j = 0; j < 6; ++j) {
+    const uint32_t idx = q + j, c = idx & 3u;
+    const uint32_t mine = c == 0 ? v0.x : c == 1 ? v0.y : c == 2 ? v0.z : v0.w;
+    T[j] = group_lane<G>(mine, idx >> 2);
+  }
   // little-endian u32 at byte h + 4k = alignbyte({T[k+1], T[k]}, rb)
   const uint32_t w0 = __builtin_amdgcn_alignbyte(T[1], T[0], rb);
   const uint32_t w2 = __builtin_amdgcn_alignbyte(T[3], T[2], rb);
@@ -175,6 +171,12 @@ __device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
 }
 
 // ------------------------------------------------------------------ kernels
+//
+// Chunk classes inside a pass: a chunk wholly inside the summed range is
+// "pure" and costs one unmasked sum4; only chunks that straddle the envelope
+// head, a header/L4 cut or the end take the masked slow path, under a branch
+// that the wave skips (s_cbranch_execz) when none of its lanes has one --
+// about two of every ~25 chunk slots for a 1500 B datagram.
 
 // Generic spans: in_cksum_skip / in_cksum_pseudo_header / in_cksum_hdr.
 struct SpanSeeds {
@@ -201,7 +203,9 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
-        acc += chunk_range_sum(v[u], rel, 0, (int)len);
+        const bool pure = rel >= 0 && rel + 16 <= (int)len;
+        acc += pure ? sum4(v[u]) : 0u;
+        if (!pure && rel < (int)len) acc += range_sum(v[u], rel, 0, (int)len);
       }
       acc = fold16(acc);
     }
@@ -219,6 +223,49 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
   }
 }
 
+// Sums of one IPv4 datagram: header [0, hl) and L4 [hl, ip_len) (absolute
+// lanes, unfolded group totals), plus the parsed header.  TX excludes the
+// ip_sum field (bytes 10..11) from the header sum.
+template <int G, bool TX>
+__device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
+                                          int lane, IpHdr &ih, bool &hdr_ok, bool &l4_ok,
+                                          uint32_t &sum_h, uint32_t &sum_l) {
+  const uint32_t c0 = off & ~15u, h = off & 15u;
+  const uint32_t nch = (h + flen + 15u) >> 4;
+  const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+  u32x4 v[kU];
+  issue_pass<G>(r, c0, nch, 0, lane, v);
+  ih = parse_ipv4<G>(v[0], h);
+  hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+  l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+  if (TX) l4_ok = l4_ok && (ih.proto == 6u || ih.proto == 17u);
+  const int hend = hdr_ok && (!TX || (ih.iplen >= ih.hl && ih.iplen <= flen)) ? (int)ih.hl : 0;
+  const int lend = l4_ok ? (int)ih.iplen : hend;
+  uint32_t acc_h = 0, acc_l = 0;
+  for (uint32_t p = 0;;) {
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+      const bool pure = rel >= hend && rel + 16 <= lend;
+      acc_l += pure ? sum4(v[u]) : 0u;
+      if (!pure && rel < lend) {
+        if (TX) {
+          // ip_sum is zeroed before in_cksum (ip_output.c:670-672)
+          acc_h += range_sum(v[u], rel, 0, min(hend, 10)) + range_sum(v[u], rel, 12, hend);
+        } else {
+          acc_h += range_sum(v[u], rel, 0, hend);
+        }
+        acc_l += range_sum(v[u], rel, hend, lend);
+      }
+    }
+    acc_l = fold16(acc_l);
+    if (++p >= npass) break;
+    issue_pass<G>(r, c0, nch, p, lane, v);
+  }
+  sum_h = group_sum<G>(fold16(acc_h));
+  sum_l = group_sum<G>(acc_l);
+}
+
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
 template <int G>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
@@ -229,43 +276,21 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
   const uint32_t stride = gridDim.x * (kBlock / G);
   for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
     const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
-    const uint32_t c0 = off & ~15u, h = off & 15u;
-    const uint32_t nch = (h + flen + 15u) >> 4;
-    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
-
-    u32x4 v[kU];
-    issue_pass<G>(r, c0, nch, 0, lane, v);
-    const IpHdr ih = parse_ipv4<G>(v[0], h);
-    const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-    const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-    const int hend = hdr_ok ? (int)ih.hl : 0;
-    const int lend = l4_ok ? (int)ih.iplen : hend;
-
-    uint32_t acc_h = 0, acc_l = 0;
-    for (uint32_t p = 0;;) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
-        acc_h += chunk_range_sum(v[u], rel, 0, hend);
-        acc_l += chunk_range_sum(v[u], rel, hend, lend);
-      }
-      acc_l = fold16(acc_l);
-      if (++p >= npass) break;
-      issue_pass<G>(r, c0, nch, p, lane, v);
-    }
-    acc_h = group_sum<G>(fold16(acc_h));
-    acc_l = group_sum<G>(acc_l);
+    IpHdr ih;
+    bool hdr_ok, l4_ok;
+    uint32_t sum_h, sum_l;
+    ipv4_sums<G, false>(r, off, flen, lane, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
       uint32_t ip = 0, l4 = 0, st = 0;
       if (!hdr_ok) {
         st = MI_ST_MALFORMED;
       } else {
-        uint32_t sh = fold16(acc_h);
+        uint32_t sh = fold16(sum_h);
         if (ih.hl != 20u && odd) sh = swap16(sh);  // in_cksum (stream) vs in_cksum_hdr (abs)
         ip = ~sh & 0xffffu;
         if (l4_ok) {
-          uint32_t sl = fold16(acc_l);
+          uint32_t sl = fold16(sum_l);
           if (odd) sl = swap16(sl);
           const uint32_t plen = ih.iplen - ih.hl;
           const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(plen);
@@ -292,39 +317,15 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
   const uint32_t stride = gridDim.x * (kBlock / G);
   for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
     const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
-    const uint32_t c0 = off & ~15u, h = off & 15u;
-    const uint32_t nch = (h + flen + 15u) >> 4;
-    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
-
-    u32x4 v[kU];
-    issue_pass<G>(r, c0, nch, 0, lane, v);
-    const IpHdr ih = parse_ipv4<G>(v[0], h);
-    const bool ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl &&
-                    ih.iplen <= flen;
-    const bool do_l4 = ok && (ih.proto == 6u || ih.proto == 17u);
-    const int hend = ok ? (int)ih.hl : 0;
-    const int lend = do_l4 ? (int)ih.iplen : hend;
-
-    uint32_t acc_h = 0, acc_l = 0;
-    for (uint32_t p = 0;;) {
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
-        // ip_sum (bytes 10..11) is zeroed before in_cksum (ip_output.c:670-672)
-        acc_h += chunk_range_sum(v[u], rel, 0, min(hend, 10)) +
-                 chunk_range_sum(v[u], rel, 12, hend);
-        acc_l += chunk_range_sum(v[u], rel, hend, lend);
-      }
-      acc_l = fold16(acc_l);
-      if (++p >= npass) break;
-      issue_pass<G>(r, c0, nch, p, lane, v);
-    }
-    acc_h = group_sum<G>(fold16(acc_h));
-    acc_l = group_sum<G>(acc_l);
+    IpHdr ih;
+    bool hdr_ok, do_l4;
+    uint32_t sum_h, sum_l;
+    ipv4_sums<G, true>(r, off, flen, lane, ih, hdr_ok, do_l4, sum_h, sum_l);
+    const bool ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
     if (lane == 0 && ok) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
       if (do_l4) {
-        uint32_t sl = fold16(acc_l);
+        uint32_t sl = fold16(sum_l);
         if (odd) sl = swap16(sl);
         uint32_t c = ~sl & 0xffffu;
         if (ih.proto == 17u && c == 0u) c = 0xffffu;
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
           __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
         }
       }
-      uint32_t sh = fold16(acc_h);
+      uint32_t sh = fold16(sum_h);
       if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
       const uint32_t c = ~sh & 0xffffu;
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t byt
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
-      acc += chunk_range_sum(v[u], rel, 0, (int)len);
+      acc += range_sum(v[u], rel, 0, (int)len);
     }
     acc = fold16(acc);
   }
@@ -464,6 +465,9 @@ struct ThreadCtx {
   uint8_t *hdesc[kRing] = {};  // same, page-locked host
   uint32_t *dbad = nullptr;
   size_t dstage_cap = 0, dout_cap = 0;
+  // repeat-launch timing events
+  hipEvent_t *ev = nullptr;
+  uint32_t nev = 0;
 };
 thread_local ThreadCtx t_ctx;
 
@@ -612,6 +616,52 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (!d.n) return 0;
   return launch_verify(d, pick_group(batch_max_len(b)), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
+}
+
+int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
+                                uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
+                                void *const *streams, uint32_t nstreams, float *kernel_us) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b || !nb) return set_err(-EINVAL, "no batches");
+  ThreadCtx &c = t_ctx;
+  Desc d[16];
+  int G[16];
+  if (nb > 16) return set_err(-EINVAL, "at most 16 batches");
+  for (uint32_t k = 0; k < nb; ++k) {
+    if ((rc = make_desc(&b[k], &d[k]))) return rc;
+    G[k] = pick_group(batch_max_len(&b[k]));
+  }
+  if (kernel_us && c.nev < 2 * steps) {
+    for (uint32_t e = 0; e < c.nev; ++e) (void)hipEventDestroy(c.ev[e]);
+    free(c.ev);
+    c.ev = (hipEvent_t *)calloc(2 * (size_t)steps, sizeof(hipEvent_t));
+    c.nev = 0;
+    if (!c.ev) return set_err(-ENOMEM, "events");
+    for (uint32_t e = 0; e < 2 * steps; ++e) {
+      HIP_TRY(hipEventCreate(&c.ev[e]));
+      c.nev = e + 1;
+    }
+  }
+  const uint32_t ns = nstreams ? nstreams : 1;
+  for (uint32_t k = 0; k < steps; ++k) {
+    const uint32_t j = k % nb;
+    hipStream_t st = nstreams ? (hipStream_t)streams[k % ns] : nullptr;
+    if (kernel_us) HIP_TRY(hipEventRecord(c.ev[2 * k], st));
+    if ((rc = launch_verify(d[j], G[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
+                            status ? status[j] : nullptr, nullptr, st)))
+      return rc;
+    if (kernel_us) HIP_TRY(hipEventRecord(c.ev[2 * k + 1], st));
+  }
+  for (uint32_t q = 0; q < ns; ++q)
+    HIP_TRY(hipStreamSynchronize(nstreams ? (hipStream_t)streams[q] : nullptr));
+  if (kernel_us)
+    for (uint32_t k = 0; k < steps; ++k) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, c.ev[2 * k], c.ev[2 * k + 1]));
+      kernel_us[k] = ms * 1000.f;
+    }
+  return 0;
 }
 
 int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {
