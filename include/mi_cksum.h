@@ -75,6 +75,12 @@ int mi_cksum_init(int device);
 const char *mi_cksum_strerror(void);
 const char *mi_cksum_version(void);
 
+/* Tuning knob (process-wide): force the lane-group shape -- `group` lanes per
+ * packet, `chunks` 16-byte loads per lane per pass -- and cap the grid at
+ * `max_blocks` workgroups.  0, 0, 0 restores the automatic choice.  Shapes
+ * change speed only, never results.  -EINVAL for a shape not compiled in. */
+int mi_cksum_set_shape(int group, int chunks, int max_blocks);
+
 /* ------------------------------------------------------------------------ */
 /* (b2) batch offload                                                         */
 /* ------------------------------------------------------------------------ */

@@ -48,7 +48,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int kBlock = 256;           // 4 waves
-constexpr int kU = 4;                 // chunks per lane per pass
+constexpr int kU = 4;                 // chunks per lane per pass (scalar path)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // offset the bounds check always rejects
 constexpr uint64_t kMaxBytes = 0xFFFFF000ull - 4096;
 
@@ -130,14 +130,14 @@ __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
-// Issue the kU loads of pass p for a packet whose envelope starts at byte c0
+// Issue the U loads of pass p for a packet whose envelope starts at byte c0
 // and has nch chunks; chunks past the envelope get the out-of-range offset.
-template <int G>
+template <int G, int U>
 __device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0, uint32_t nch,
-                                           uint32_t p, int lane, u32x4 (&v)[kU]) {
+                                           uint32_t p, int lane, u32x4 (&v)[U]) {
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    const uint32_t ci = p * (G * kU) + u * G + lane;
+  for (int u = 0; u < U; ++u) {
+    const uint32_t ci = p * (G * U) + u * G + lane;
     v[u] = ld16(r, ci < nch ? c0 + 16u * ci : kOOB);
   }
 }
@@ -185,7 +185,7 @@ struct SpanSeeds {
   const uint32_t *plens;
 };
 
-template <int G>
+template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, SpanSeeds s,
                                                  uint16_t *out) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
@@ -195,14 +195,14 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
     const uint32_t off = pkt_off(d, i), len = pkt_len(d, i);
     const uint32_t c0 = off & ~15u, h = off & 15u;
     const uint32_t nch = len ? (h + len + 15u) >> 4 : 0u;
-    const uint32_t npass = (nch + G * kU - 1) / (G * kU);
+    const uint32_t npass = (nch + G * U - 1) / (G * U);
     uint32_t acc = 0;
     for (uint32_t p = 0; p < npass; ++p) {
-      u32x4 v[kU];
-      issue_pass<G>(r, c0, nch, p, lane, v);
+      u32x4 v[U];
+      issue_pass<G, U>(r, c0, nch, p, lane, v);
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+      for (int u = 0; u < U; ++u) {
+        const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
         const bool pure = rel >= 0 && rel + 16 <= (int)len;
         acc += pure ? sum4(v[u]) : 0u;
         if (!pure && rel < (int)len) acc += range_sum(v[u], rel, 0, (int)len);
@@ -226,15 +226,15 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
 // Sums of one IPv4 datagram: header [0, hl) and L4 [hl, ip_len) (absolute
 // lanes, unfolded group totals), plus the parsed header.  TX excludes the
 // ip_sum field (bytes 10..11) from the header sum.
-template <int G, bool TX>
+template <int G, int U, bool TX>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                           int lane, IpHdr &ih, bool &hdr_ok, bool &l4_ok,
                                           uint32_t &sum_h, uint32_t &sum_l) {
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = (h + flen + 15u) >> 4;
-  const uint32_t npass = (nch + G * kU - 1) / (G * kU);
-  u32x4 v[kU];
-  issue_pass<G>(r, c0, nch, 0, lane, v);
+  const uint32_t npass = (nch + G * U - 1) / (G * U);
+  u32x4 v[U];
+  issue_pass<G, U>(r, c0, nch, 0, lane, v);
   ih = parse_ipv4<G>(v[0], h);
   hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
   l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
@@ -244,8 +244,8 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   uint32_t acc_h = 0, acc_l = 0;
   for (uint32_t p = 0;;) {
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
+    for (int u = 0; u < U; ++u) {
+      const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
       const bool pure = rel >= hend && rel + 16 <= lend;
       acc_l += pure ? sum4(v[u]) : 0u;
       if (!pure && rel < lend) {
@@ -260,14 +260,14 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
     }
     acc_l = fold16(acc_l);
     if (++p >= npass) break;
-    issue_pass<G>(r, c0, nch, p, lane, v);
+    issue_pass<G, U>(r, c0, nch, p, lane, v);
   }
   sum_h = group_sum<G>(fold16(acc_h));
   sum_l = group_sum<G>(acc_l);
 }
 
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
-template <int G>
+template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
                                                         uint16_t *l4_out, uint8_t *st_out,
                                                         uint32_t *bad) {
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
     IpHdr ih;
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, false>(r, off, flen, lane, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    ipv4_sums<G, U, false>(r, off, flen, lane, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
       uint32_t ip = 0, l4 = 0, st = 0;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
 // (ip_output.c:667-672).
-template <int G>
+template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
     IpHdr ih;
     bool hdr_ok, do_l4;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, true>(r, off, flen, lane, ih, hdr_ok, do_l4, sum_h, sum_l);
+    ipv4_sums<G, U, true>(r, off, flen, lane, ih, hdr_ok, do_l4, sum_h, sum_l);
     const bool ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
     if (lane == 0 && ok) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t byt
   uint32_t acc = 0;
   for (uint32_t p = 0; p < npass; ++p) {
     u32x4 v[kU];
-    issue_pass<G>(r, c0, nch, p, lane, v);
+    issue_pass<G, kU>(r, c0, nch, p, lane, v);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int rel = (int)(16u * (p * (G * kU) + u * G + lane)) - (int)h;
@@ -496,23 +496,58 @@ int ensure_ctx() {
   return 0;
 }
 
-int pick_group(uint32_t max_len) {
+// Lane-group shape (G lanes per packet, U chunk loads per lane per pass).
+// Every shape is correct for every length (long packets loop over passes);
+// the shape only sets how many bytes a wave keeps in flight and how many slots
+// go unused.  FOR_GU lists the instantiated shapes.
+#define FOR_GU(X)                                                                  \
+  X(4, 1) X(4, 2) X(4, 4) X(8, 2) X(8, 4) X(8, 8) X(8, 12) X(16, 2) X(16, 4)       \
+  X(16, 6) X(16, 8) X(32, 2) X(32, 3) X(32, 4) X(32, 6) X(64, 2) X(64, 3) X(64, 4) \
+  X(64, 6) X(64, 9)
+
+struct Shape {
+  int g, u;
+};
+
+bool shape_ok(int g, int u) {
+#define X(G_, U_) if (g == G_ && u == U_) return true;
+  FOR_GU(X)
+#undef X
+  return false;
+}
+
+struct Tuning {
+  int g = 0, u = 0, max_blocks = 0;
+};
+Tuning g_tune = [] {
+  Tuning t;
+  if (const char *s = getenv("MI_CKSUM_SHAPE")) {  // "GxU"
+    int g = 0, u = 0;
+    if (sscanf(s, "%dx%d", &g, &u) == 2 && shape_ok(g, u)) t.g = g, t.u = u;
+  }
+  if (const char *s = getenv("MI_CKSUM_MAX_BLOCKS")) t.max_blocks = atoi(s);
+  return t;
+}();
+
+Shape pick_shape(uint32_t max_len) {
+  if (g_tune.g) return {g_tune.g, g_tune.u};
   // chunks of the 16-byte envelope, worst-case misalignment
   const uint32_t ch = (max_len + 15u + 15u) / 16u;
-  const uint32_t per = (ch + kU - 1) / kU;
-  if (per <= 4) return 4;
-  if (per <= 8) return 8;
-  if (per <= 16) return 16;
-  if (per <= 32) return 32;
-  return 64;
+  if (ch <= 4) return {4, 1};
+  if (ch <= 8) return {4, 2};
+  if (ch <= 16) return {4, 4};
+  if (ch <= 32) return {8, 4};
+  if (ch <= 64) return {8, 8};
+  if (ch <= 96) return {32, 3};
+  if (ch <= 128) return {32, 4};
+  if (ch <= 192) return {32, 6};
+  if (ch <= 256) return {64, 4};
+  if (ch <= 384) return {64, 6};
+  return {64, 9};
 }
 
 int grid_for(uint32_t n, int G) {
-  static int cap = [] {
-    const char *s = getenv("MI_CKSUM_MAX_BLOCKS");
-    int v = s ? atoi(s) : 0;
-    return v > 0 ? v : 4096;
-  }();
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 4096;
   const uint64_t groups_per_block = kBlock / G;
   uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
   if (blocks > (uint64_t)cap) blocks = cap;
@@ -546,21 +581,48 @@ uint32_t batch_max_len(const mi_pkt_batch *b) {
   return b->max_len ? b->max_len : 1500u;
 }
 
-#define DISPATCH_G(G, CALL)                 \
-  switch (G) {                              \
-    case 4: { constexpr int kG = 4; CALL; } break;   \
-    case 8: { constexpr int kG = 8; CALL; } break;   \
-    case 16: { constexpr int kG = 16; CALL; } break; \
-    case 32: { constexpr int kG = 32; CALL; } break; \
-    default: { constexpr int kG = 64; CALL; } break; \
-  }
-
-int launch_verify(const Desc &d, int G, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad,
-                  hipStream_t s) {
-  const int grid = grid_for(d.n, G);
-  DISPATCH_G(G, hipLaunchKernelGGL(k_ipv4_verify<kG>, dim3(grid), dim3(kBlock), 0, s, d, ip, l4, st, bad));
+int launched() {
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+int launch_verify(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad,
+                  hipStream_t s) {
+  const int grid = grid_for(d.n, sh.g);
+#define X(G_, U_)                                                                        \
+  if (sh.g == G_ && sh.u == U_) {                                                        \
+    hipLaunchKernelGGL((k_ipv4_verify<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d, ip, l4, \
+                       st, bad);                                                         \
+    return launched();                                                                   \
+  }
+  FOR_GU(X)
+#undef X
+  return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
+}
+
+int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd, uint16_t *out,
+                hipStream_t s) {
+  const int grid = grid_for(d.n, sh.g);
+#define X(G_, U_)                                                                          \
+  if (sh.g == G_ && sh.u == U_) {                                                          \
+    hipLaunchKernelGGL((k_span<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d, abs_lanes, sd, out); \
+    return launched();                                                                     \
+  }
+  FOR_GU(X)
+#undef X
+  return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
+}
+
+int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
+  const int grid = grid_for(d.n, sh.g);
+#define X(G_, U_)                                                                  \
+  if (sh.g == G_ && sh.u == U_) {                                                  \
+    hipLaunchKernelGGL((k_ipv4_finalize<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d); \
+    return launched();                                                             \
+  }
+  FOR_GU(X)
+#undef X
+  return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
 }
 
 }  // namespace
@@ -584,6 +646,16 @@ int mi_cksum_init(int device) {
   return ensure_ctx();
 }
 
+int mi_cksum_set_shape(int group, int chunks, int max_blocks) {
+  if (group || chunks) {
+    if (!shape_ok(group, chunks)) return set_err(-EINVAL, "no kernel for shape %dx%d", group, chunks);
+  }
+  g_tune.g = group;
+  g_tune.u = group ? chunks : 0;
+  g_tune.max_blocks = max_blocks > 0 ? max_blocks : 0;
+  return 0;
+}
+
 int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_seeds *seeds,
                         uint16_t *out, void *stream) {
   Desc d;
@@ -598,13 +670,8 @@ int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_see
     s.proto = seeds->proto; s.plens = seeds->plens;
     if (s.src && (!s.dst || !s.proto)) return set_err(-EINVAL, "src without dst/proto");
   }
-  const int G = pick_group(batch_max_len(b));
-  const int grid = grid_for(d.n, G);
   const uint32_t abs_lanes = lanes == MI_SPAN_ABS;
-  hipStream_t st = (hipStream_t)stream;
-  DISPATCH_G(G, hipLaunchKernelGGL(k_span<kG>, dim3(grid), dim3(kBlock), 0, st, d, abs_lanes, s, out));
-  HIP_TRY(hipGetLastError());
-  return 0;
+  return launch_span(d, pick_shape(batch_max_len(b)), abs_lanes, s, out, (hipStream_t)stream);
 }
 
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
@@ -614,7 +681,7 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (rc) return rc;
   if ((rc = make_desc(b, &d))) return rc;
   if (!d.n) return 0;
-  return launch_verify(d, pick_group(batch_max_len(b)), ip_sum, l4_sum, status, bad_count,
+  return launch_verify(d, pick_shape(batch_max_len(b)), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
 }
 
@@ -626,11 +693,11 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
   if (!b || !nb) return set_err(-EINVAL, "no batches");
   ThreadCtx &c = t_ctx;
   Desc d[16];
-  int G[16];
+  Shape G[16];
   if (nb > 16) return set_err(-EINVAL, "at most 16 batches");
   for (uint32_t k = 0; k < nb; ++k) {
     if ((rc = make_desc(&b[k], &d[k]))) return rc;
-    G[k] = pick_group(batch_max_len(&b[k]));
+    G[k] = pick_shape(batch_max_len(&b[k]));
   }
   if (kernel_us && c.nev < 2 * steps) {
     for (uint32_t e = 0; e < c.nev; ++e) (void)hipEventDestroy(c.ev[e]);
@@ -670,12 +737,7 @@ int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {
   if (rc) return rc;
   if ((rc = make_desc(b, &d))) return rc;
   if (!d.n) return 0;
-  const int G = pick_group(batch_max_len(b));
-  const int grid = grid_for(d.n, G);
-  hipStream_t st = (hipStream_t)stream;
-  DISPATCH_G(G, hipLaunchKernelGGL(k_ipv4_finalize<kG>, dim3(grid), dim3(kBlock), 0, st, d));
-  HIP_TRY(hipGetLastError());
-  return 0;
+  return launch_finalize(d, pick_shape(batch_max_len(b)), (hipStream_t)stream);
 }
 
 int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
@@ -787,7 +849,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
   HIP_TRY(hipMemsetAsync(c.dbad, 0, 4 * ThreadCtx::kRing, c.hstream[0]));
   HIP_TRY(hipStreamSynchronize(c.hstream[0]));
 
-  const int G = pick_group(max_len);
+  const Shape G = pick_shape(max_len);
   bool used[ThreadCtx::kRing] = {};
   int k = 0;
   for (uint32_t i = 0; i < b->n;) {
