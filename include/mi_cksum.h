@@ -161,13 +161,15 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
  * verify passes, pass k over batch b[k % nb] with outputs ip/l4/status[k % nb]
  * (arrays of nb device pointers; any array may be NULL), on
  * streams[k % nstreams] (nstreams = 0: the default stream).  If kernel_us is
- * non-NULL each pass is bracketed by hipEvents on its own stream and
- * kernel_us[k] gets its duration.  Synchronous: returns once every pass has
- * finished.  nb <= 16.
+ * non-NULL each pass is bracketed by hipEvents on its own stream, kernel_us[k]
+ * gets its duration and *span_us (may be NULL) the time from the first pass's
+ * start to the last end, i.e. the GPU time of all passes, overlap included.
+ * Synchronous: returns once every pass has finished.  nb <= 16.
  */
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
                                 uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
-                                void *const *streams, uint32_t nstreams, float *kernel_us);
+                                void *const *streams, uint32_t nstreams, float *kernel_us,
+                                float *span_us);
 
 /*
  * TX finalize in place (ip_output.c:649-672 + in_delayed_cksum :958-983):

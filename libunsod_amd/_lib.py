@@ -68,7 +68,8 @@ SIGNATURES = {
     "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
     "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
-                                              C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_float)]),
+                                              C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_float),
+                                              C.POINTER(C.c_float)]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),

@@ -175,8 +175,9 @@ def span_batch(b: PktBatch, lanes: int = MI_SPAN_STREAM, *, seeds=None, src=None
 def ipv4_verify_repeat(batches, outs, steps: int, streams=None, timing: bool = True):
     """Launch ``steps`` verify passes back to back from native code (pass k over
     batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on
-    streams[k % len(streams)] or the current stream).  Synchronous; returns the
-    per-pass kernel durations in microseconds (hipEvents) or None."""
+    streams[k % len(streams)] or the current stream).  Synchronous.  With
+    ``timing`` returns (per-pass kernel durations in us, GPU span of all passes
+    in us) from hipEvents, else None."""
     nb = len(batches)
     arr = (PktBatchC * nb)(*[b.c for b in batches])
     VP = C.c_void_p * nb
@@ -185,10 +186,13 @@ def ipv4_verify_repeat(batches, outs, steps: int, streams=None, timing: bool = T
         streams = [None]
     sh = (C.c_void_p * len(streams))(*[_stream(x) for x in streams])
     us = (C.c_float * steps)() if timing else None
+    span = C.c_float(0.0)
     check("mi_cksum_ipv4_verify_repeat",
           load().mi_cksum_ipv4_verify_repeat(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], steps, sh,
-                                             len(streams), us))
-    return None if us is None else np.frombuffer(us, dtype=np.float32).copy()
+                                             len(streams), us, C.byref(span) if timing else None))
+    if not timing:
+        return None
+    return np.frombuffer(us, dtype=np.float32).copy(), float(span.value)
 
 
 def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:

@@ -531,6 +531,11 @@ Tuning g_tune = [] {
   return t;
 }();
 
+// Measured on MI355X (tools/sweep.py, profiles/): narrow groups win -- a wave
+// folds 8-16 datagrams at once, so per-packet fixed costs (header broadcast,
+// butterfly, store) are shared and each lane streams several passes.  1500 B:
+// 8x4 / 8x2 = 20.1 us vs 32x3 26 us and 64x4 46 us; 9000 B: every shape is
+// within 1 % of 8x12 (bandwidth-bound).
 Shape pick_shape(uint32_t max_len) {
   if (g_tune.g) return {g_tune.g, g_tune.u};
   // chunks of the 16-byte envelope, worst-case misalignment
@@ -538,14 +543,9 @@ Shape pick_shape(uint32_t max_len) {
   if (ch <= 4) return {4, 1};
   if (ch <= 8) return {4, 2};
   if (ch <= 16) return {4, 4};
-  if (ch <= 32) return {8, 4};
-  if (ch <= 64) return {8, 8};
-  if (ch <= 96) return {32, 3};
-  if (ch <= 128) return {32, 4};
-  if (ch <= 192) return {32, 6};
-  if (ch <= 256) return {64, 4};
-  if (ch <= 384) return {64, 6};
-  return {64, 9};
+  if (ch <= 128) return {8, 4};
+  if (ch <= 256) return {8, 8};
+  return {8, 12};
 }
 
 int grid_for(uint32_t n, int G) {
@@ -689,7 +689,8 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
 
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
                                 uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
-                                void *const *streams, uint32_t nstreams, float *kernel_us) {
+                                void *const *streams, uint32_t nstreams, float *kernel_us,
+                                float *span_us) {
   int rc = ensure_ctx();
   if (rc) return rc;
   if (!b || !nb) return set_err(-EINVAL, "no batches");
@@ -724,12 +725,17 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
   }
   for (uint32_t q = 0; q < ns; ++q)
     HIP_TRY(hipStreamSynchronize(nstreams ? (hipStream_t)streams[q] : nullptr));
-  if (kernel_us)
+  if (kernel_us) {
+    float span = 0.f;
     for (uint32_t k = 0; k < steps; ++k) {
-      float ms = 0.f;
+      float ms = 0.f, end = 0.f;
       HIP_TRY(hipEventElapsedTime(&ms, c.ev[2 * k], c.ev[2 * k + 1]));
+      HIP_TRY(hipEventElapsedTime(&end, c.ev[0], c.ev[2 * k + 1]));
       kernel_us[k] = ms * 1000.f;
+      if (end > span) span = end;
     }
+    if (span_us) *span_us = span * 1000.f;
+  }
   return 0;
 }
 

@@ -239,3 +239,11 @@ def test_deterministic_and_stream_async():
     for k in ("ip", "l4", "status"):
         assert np.array_equal(cpu(r1[k]), cpu(r2[k]))
     assert not cpu(r1["status"]).any()
+    # the native back-to-back launcher writes the same outputs, on two streams
+    outs = [dict(ip=torch.full((n,), 7, dtype=torch.int16, device="cuda").view(torch.uint16),
+                 l4=torch.full((n,), 7, dtype=torch.int16, device="cuda").view(torch.uint16),
+                 status=torch.full((n,), 9, dtype=torch.uint8, device="cuda"))]
+    us, span = mi.ipv4_verify_repeat([b], outs, 6, streams=[torch.cuda.current_stream(), torch.cuda.Stream()])
+    assert us.shape == (6,) and (us > 0).all() and span >= us.max() * 0.99
+    for k in ("ip", "l4", "status"):
+        assert np.array_equal(cpu(outs[0][k]), cpu(r1[k]))

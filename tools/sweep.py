@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--configs", default="1500,9000,64,pareto")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--grids", default="0,1024,2048,8192,16384")
-    ap.add_argument("--streams", default="1,2")
+    ap.add_argument("--streams", default="1,2,3,4")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for cfg in a.configs.split(","):
@@ -80,8 +80,11 @@ def main():
                     mi.ipv4_verify_repeat(bs, outs, 20, streams=streams, timing=False)
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                    us = mi.ipv4_verify_repeat(bs, outs, a.steps, streams=streams, timing=True)
+                    us, span = mi.ipv4_verify_repeat(bs, outs, a.steps, streams=streams, timing=True)
                     dt = time.perf_counter() - t0
+                    t1 = time.perf_counter()
+                    mi.ipv4_verify_repeat(bs, outs, a.steps, streams=streams, timing=False)
+                    dt_noev = time.perf_counter() - t1
                     chk = mi.ipv4_verify(bs[0], bad_count=True)
                     torch.cuda.synchronize()
                     ok = int(chk["bad"].item()) == 0
@@ -89,8 +92,10 @@ def main():
                     print(json.dumps(dict(config=cfg, g=g, u=u, grid=grid, streams=ns, kern_us=round(med, 2),
                                           kern_min_us=round(float(us.min()), 2),
                                           GBps=round((lsum + 5 * n) / med / 1e3, 1),
-                                          step_us=round(dt / a.steps * 1e6, 2),
-                                          job_GiBps=round(lsum * a.steps / dt / 2**30, 1), ok=ok)), flush=True)
+                                          step_us=round(dt / a.steps * 1e6, 2), gpu_us_per_launch=round(span / a.steps, 2),
+                                          job_GiBps=round(lsum * a.steps / dt / 2**30, 1),
+                                          job_GiBps_noev=round(lsum * a.steps / dt_noev / 2**30, 1), ok=ok)),
+                          flush=True)
         mi.set_shape(0, 0, 0)
         del bs, outs
         torch.cuda.empty_cache()
