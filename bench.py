@@ -125,20 +125,19 @@ def main():
         raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
 
     nst = max(1, args.streams)
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nst - 1)]
-    mi.ipv4_verify_repeat(batches, outs, args.warmup, streams=streams, timing=False)
+    mi.ipv4_verify_repeat(batches, outs, args.warmup, nstreams=nst, timing="none")
     torch.cuda.synchronize()
 
     # ------------------------------------------------------- timed region
     # K launches issued back to back from native code (libmicksum), alternating
-    # over `nst` streams so that a launch's ramp-up overlaps its predecessor's
-    # drain; each launch is bracketed by hipEvents on the stream it runs on.
+    # over `nst` non-blocking streams so that a launch's ramp-up overlaps its
+    # predecessor's drain; a hipEvent pair per stream brackets the region.
     K = args.steps
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kern_us, span_us = mi.ipv4_verify_repeat(batches, outs, K, streams=streams, timing=True)
+    span_us = mi.ipv4_verify_repeat(batches, outs, K, nstreams=nst, timing="region")
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
@@ -161,9 +160,10 @@ def main():
 
     # Roofline of the dominant kernel (k_ipv4_verify).  Algorithmic bytes per
     # launch = sum(L) read + 5 B written per packet (ip u16, l4 u16, status u8).
-    # GPU time per launch = (last launch end - first launch start) / K from the
-    # hipEvents above: launches on different streams overlap, so the per-launch
-    # event durations (kept as overlapped_launch_us) double-count the shared time.
+    # Average launch duration = GPU span of the timed region (hipEvents on the
+    # launch streams) / K: launches on different streams overlap, so this is the
+    # GPU time each launch costs; rocprof's union of dispatch intervals / K is
+    # the same quantity (tools/prof_summary.py).
     gpu_s_per_launch = span_us / K / 1e6
     alg_bytes = float(L_sum) + 5.0 * n
     achieved = alg_bytes / gpu_s_per_launch / 1e9
@@ -177,11 +177,10 @@ def main():
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
                 kernel="k_ipv4_verify", alg_bytes_per_launch=int(alg_bytes),
-                avg_launch_us=round(gpu_s_per_launch * 1e6, 2),
-                overlapped_launch_us=round(float(np.mean(kern_us)), 2), streams=nst)
-    # the same kernel alone on one stream (no overlap), for comparison with a
-    # single-stream rocprof trace
-    iso_us, iso_span = mi.ipv4_verify_repeat(batches, outs, min(K, 100), streams=streams[:1], timing=True)
+                avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst)
+    # the same kernel alone on one stream, every launch bracketed by events
+    # (compare with a single-stream rocprof trace)
+    iso_us, _ = mi.ipv4_verify_repeat(batches, outs, min(K, 100), nstreams=1, timing="pass")
     roof["isolated_launch_us"] = round(float(np.median(iso_us)), 2)
     roof["isolated_achieved"] = round(alg_bytes / (float(np.median(iso_us)) / 1e6) / 1e9, 1)
 

@@ -159,16 +159,22 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
 /*
  * Back-to-back submission (the RX burst loop, and the bench): launch `steps`
  * verify passes, pass k over batch b[k % nb] with outputs ip/l4/status[k % nb]
- * (arrays of nb device pointers; any array may be NULL), on
- * streams[k % nstreams] (nstreams = 0: the default stream).  If kernel_us is
- * non-NULL each pass is bracketed by hipEvents on its own stream, kernel_us[k]
- * gets its duration and *span_us (may be NULL) the time from the first pass's
- * start to the last end, i.e. the GPU time of all passes, overlap included.
+ * (arrays of nb device pointers; any array may be NULL), on the k % nstreams-th
+ * of nstreams (1..8) library-owned non-blocking streams, so consecutive passes
+ * can overlap (a pass's ramp-up runs under its predecessor's drain).  The passes
+ * start after all work already queued on the legacy default stream.
+ * timing: MI_TIME_NONE; MI_TIME_REGION -- one hipEvent before the first pass
+ * and one after the last pass on every stream, *span_us = GPU time of all
+ * passes; MI_TIME_PER_PASS -- every pass bracketed by events on its stream,
+ * kernel_us[k] = its duration (overlap included) and *span_us as above.
  * Synchronous: returns once every pass has finished.  nb <= 16.
  */
+#define MI_TIME_NONE     0u
+#define MI_TIME_REGION   1u
+#define MI_TIME_PER_PASS 2u
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
                                 uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
-                                void *const *streams, uint32_t nstreams, float *kernel_us,
+                                uint32_t nstreams, uint32_t timing, float *kernel_us,
                                 float *span_us);
 
 /*

@@ -18,6 +18,9 @@ MI_SPAN_ABS = 1
 MI_ST_IP_BAD = 1
 MI_ST_L4_BAD = 2
 MI_ST_MALFORMED = 4
+MI_TIME_NONE = 0
+MI_TIME_REGION = 1
+MI_TIME_PER_PASS = 2
 
 
 class MiCksumError(RuntimeError):
@@ -68,7 +71,7 @@ SIGNATURES = {
     "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
     "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
-                                              C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_float),
+                                              C.c_uint32, C.c_uint32, C.POINTER(C.c_float),
                                               C.POINTER(C.c_float)]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),

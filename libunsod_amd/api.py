@@ -17,7 +17,8 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_SPAN_ABS, MI_SPAN_STREAM, PktBatchC, SpanSeedsC, check, load)
+from ._lib import (MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+                   SpanSeedsC, check, load)
 
 MSIZE = 256  # param.h:159
 
@@ -172,26 +173,28 @@ def span_batch(b: PktBatch, lanes: int = MI_SPAN_STREAM, *, seeds=None, src=None
     return out
 
 
-def ipv4_verify_repeat(batches, outs, steps: int, streams=None, timing: bool = True):
-    """Launch ``steps`` verify passes back to back from native code (pass k over
-    batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on
-    streams[k % len(streams)] or the current stream).  Synchronous.  With
-    ``timing`` returns (per-pass kernel durations in us, GPU span of all passes
-    in us) from hipEvents, else None."""
+def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str = "region"):
+    """Launch ``steps`` verify passes back to back from native code: pass k over
+    batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on the library's
+    k % nstreams-th non-blocking stream.  Synchronous.
+
+    timing="none" -> None; "region" -> GPU span of all passes in us (one
+    hipEvent pair around the region per stream); "pass" -> (per-pass durations
+    in us, span in us), events around every pass."""
+    mode = {"none": MI_TIME_NONE, "region": MI_TIME_REGION, "pass": MI_TIME_PER_PASS}[timing]
     nb = len(batches)
     arr = (PktBatchC * nb)(*[b.c for b in batches])
     VP = C.c_void_p * nb
     ptrs = {k: VP(*[_ptr(o.get(k)) for o in outs]) for k in ("ip", "l4", "status")}
-    if streams is None:
-        streams = [None]
-    sh = (C.c_void_p * len(streams))(*[_stream(x) for x in streams])
-    us = (C.c_float * steps)() if timing else None
+    us = (C.c_float * steps)() if mode == MI_TIME_PER_PASS else None
     span = C.c_float(0.0)
     check("mi_cksum_ipv4_verify_repeat",
-          load().mi_cksum_ipv4_verify_repeat(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], steps, sh,
-                                             len(streams), us, C.byref(span) if timing else None))
-    if not timing:
+          load().mi_cksum_ipv4_verify_repeat(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], steps, nstreams,
+                                             mode, us, C.byref(span)))
+    if mode == MI_TIME_NONE:
         return None
+    if mode == MI_TIME_REGION:
+        return float(span.value)
     return np.frombuffer(us, dtype=np.float32).copy(), float(span.value)
 
 

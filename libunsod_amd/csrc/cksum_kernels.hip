@@ -467,7 +467,10 @@ struct ThreadCtx {
   uint8_t *hdesc[kRing] = {};  // same, page-locked host
   uint32_t *dbad = nullptr;
   size_t dstage_cap = 0, dout_cap = 0;
-  // repeat-launch timing events
+  // repeat-launch streams and timing events
+  static constexpr int kMaxRep = 8;
+  hipStream_t rstream[kMaxRep] = {};
+  hipEvent_t rgate = nullptr;
   hipEvent_t *ev = nullptr;
   uint32_t nev = 0;
 };
@@ -689,44 +692,59 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
 
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
                                 uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
-                                void *const *streams, uint32_t nstreams, float *kernel_us,
+                                uint32_t nstreams, uint32_t timing, float *kernel_us,
                                 float *span_us) {
   int rc = ensure_ctx();
   if (rc) return rc;
   if (!b || !nb) return set_err(-EINVAL, "no batches");
+  if (nb > 16) return set_err(-EINVAL, "at most 16 batches");
+  if (nstreams < 1 || nstreams > ThreadCtx::kMaxRep) return set_err(-EINVAL, "nstreams 1..%d", ThreadCtx::kMaxRep);
+  if (timing == MI_TIME_PER_PASS && !kernel_us) return set_err(-EINVAL, "kernel_us is NULL");
   ThreadCtx &c = t_ctx;
   Desc d[16];
   Shape G[16];
-  if (nb > 16) return set_err(-EINVAL, "at most 16 batches");
   for (uint32_t k = 0; k < nb; ++k) {
     if ((rc = make_desc(&b[k], &d[k]))) return rc;
     G[k] = pick_shape(batch_max_len(&b[k]));
   }
-  if (kernel_us && c.nev < 2 * steps) {
+  // library-owned non-blocking streams: never implicitly serialised against
+  // each other or against the legacy default stream
+  for (uint32_t q = 0; q < nstreams; ++q)
+    if (!c.rstream[q]) HIP_TRY(hipStreamCreateWithFlags(&c.rstream[q], hipStreamNonBlocking));
+  const uint32_t need_ev = timing == MI_TIME_PER_PASS ? 2 * steps : 2 + nstreams;
+  if (c.nev < need_ev) {
     for (uint32_t e = 0; e < c.nev; ++e) (void)hipEventDestroy(c.ev[e]);
     free(c.ev);
-    c.ev = (hipEvent_t *)calloc(2 * (size_t)steps, sizeof(hipEvent_t));
     c.nev = 0;
+    c.ev = (hipEvent_t *)calloc(need_ev, sizeof(hipEvent_t));
     if (!c.ev) return set_err(-ENOMEM, "events");
-    for (uint32_t e = 0; e < 2 * steps; ++e) {
+    for (uint32_t e = 0; e < need_ev; ++e) {
       HIP_TRY(hipEventCreate(&c.ev[e]));
       c.nev = e + 1;
     }
   }
-  const uint32_t ns = nstreams ? nstreams : 1;
+  if (!c.rgate) HIP_TRY(hipEventCreateWithFlags(&c.rgate, hipEventDisableTiming));
+  // order after everything already queued on the legacy default stream
+  HIP_TRY(hipEventRecord(c.rgate, nullptr));
+  for (uint32_t q = 0; q < nstreams; ++q) HIP_TRY(hipStreamWaitEvent(c.rstream[q], c.rgate, 0));
+  if (timing == MI_TIME_REGION) {
+    HIP_TRY(hipEventRecord(c.ev[0], c.rstream[0]));
+    for (uint32_t q = 1; q < nstreams; ++q) HIP_TRY(hipStreamWaitEvent(c.rstream[q], c.ev[0], 0));
+  }
   for (uint32_t k = 0; k < steps; ++k) {
     const uint32_t j = k % nb;
-    hipStream_t st = nstreams ? (hipStream_t)streams[k % ns] : nullptr;
-    if (kernel_us) HIP_TRY(hipEventRecord(c.ev[2 * k], st));
+    hipStream_t st = c.rstream[k % nstreams];
+    if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k], st));
     if ((rc = launch_verify(d[j], G[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
                             status ? status[j] : nullptr, nullptr, st)))
       return rc;
-    if (kernel_us) HIP_TRY(hipEventRecord(c.ev[2 * k + 1], st));
+    if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k + 1], st));
   }
-  for (uint32_t q = 0; q < ns; ++q)
-    HIP_TRY(hipStreamSynchronize(nstreams ? (hipStream_t)streams[q] : nullptr));
-  if (kernel_us) {
-    float span = 0.f;
+  if (timing == MI_TIME_REGION)
+    for (uint32_t q = 0; q < nstreams; ++q) HIP_TRY(hipEventRecord(c.ev[2 + q], c.rstream[q]));
+  for (uint32_t q = 0; q < nstreams; ++q) HIP_TRY(hipStreamSynchronize(c.rstream[q]));
+  float span = 0.f;
+  if (timing == MI_TIME_PER_PASS) {
     for (uint32_t k = 0; k < steps; ++k) {
       float ms = 0.f, end = 0.f;
       HIP_TRY(hipEventElapsedTime(&ms, c.ev[2 * k], c.ev[2 * k + 1]));
@@ -734,8 +752,14 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
       kernel_us[k] = ms * 1000.f;
       if (end > span) span = end;
     }
-    if (span_us) *span_us = span * 1000.f;
+  } else if (timing == MI_TIME_REGION) {
+    for (uint32_t q = 0; q < nstreams; ++q) {
+      float end = 0.f;
+      HIP_TRY(hipEventElapsedTime(&end, c.ev[0], c.ev[2 + q]));
+      if (end > span) span = end;
+    }
   }
+  if (span_us) *span_us = span * 1000.f;
   return 0;
 }
 

@@ -243,7 +243,8 @@ def test_deterministic_and_stream_async():
     outs = [dict(ip=torch.full((n,), 7, dtype=torch.int16, device="cuda").view(torch.uint16),
                  l4=torch.full((n,), 7, dtype=torch.int16, device="cuda").view(torch.uint16),
                  status=torch.full((n,), 9, dtype=torch.uint8, device="cuda"))]
-    us, span = mi.ipv4_verify_repeat([b], outs, 6, streams=[torch.cuda.current_stream(), torch.cuda.Stream()])
+    us, span = mi.ipv4_verify_repeat([b], outs, 6, nstreams=2, timing="pass")
     assert us.shape == (6,) and (us > 0).all() and span >= us.max() * 0.99
+    assert mi.ipv4_verify_repeat([b], outs, 6, nstreams=3, timing="region") > 0
     for k in ("ip", "l4", "status"):
         assert np.array_equal(cpu(outs[0][k]), cpu(r1[k]))

@@ -75,27 +75,22 @@ def main():
                 continue
             for grid in [int(x) for x in a.grids.split(",")]:
                 mi.set_shape(g, u, grid)
+                iso, _ = mi.ipv4_verify_repeat(bs, outs, 60, nstreams=1, timing="pass")
                 for ns in [int(x) for x in a.streams.split(",")]:
-                    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(ns - 1)]
-                    mi.ipv4_verify_repeat(bs, outs, 20, streams=streams, timing=False)
+                    mi.ipv4_verify_repeat(bs, outs, 20, nstreams=ns, timing="none")
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                    us, span = mi.ipv4_verify_repeat(bs, outs, a.steps, streams=streams, timing=True)
+                    span = mi.ipv4_verify_repeat(bs, outs, a.steps, nstreams=ns, timing="region")
                     dt = time.perf_counter() - t0
-                    t1 = time.perf_counter()
-                    mi.ipv4_verify_repeat(bs, outs, a.steps, streams=streams, timing=False)
-                    dt_noev = time.perf_counter() - t1
                     chk = mi.ipv4_verify(bs[0], bad_count=True)
                     torch.cuda.synchronize()
                     ok = int(chk["bad"].item()) == 0
-                    med = float(np.median(us))
-                    print(json.dumps(dict(config=cfg, g=g, u=u, grid=grid, streams=ns, kern_us=round(med, 2),
-                                          kern_min_us=round(float(us.min()), 2),
-                                          GBps=round((lsum + 5 * n) / med / 1e3, 1),
-                                          step_us=round(dt / a.steps * 1e6, 2), gpu_us_per_launch=round(span / a.steps, 2),
-                                          job_GiBps=round(lsum * a.steps / dt / 2**30, 1),
-                                          job_GiBps_noev=round(lsum * a.steps / dt_noev / 2**30, 1), ok=ok)),
-                          flush=True)
+                    med = float(np.median(iso))
+                    print(json.dumps(dict(config=cfg, g=g, u=u, grid=grid, streams=ns, iso_kern_us=round(med, 2),
+                                          iso_GBps=round((lsum + 5 * n) / med / 1e3, 1),
+                                          gpu_us_per_launch=round(span / a.steps, 2),
+                                          step_us=round(dt / a.steps * 1e6, 2),
+                                          job_GiBps=round(lsum * a.steps / dt / 2**30, 1), ok=ok)), flush=True)
         mi.set_shape(0, 0, 0)
         del bs, outs
         torch.cuda.empty_cache()
