@@ -142,20 +142,8 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tot = torch.tensor([float(L_sum)], dtype=torch.float64, device=dev)
-        dist.all_reduce(tot)
-        job_bytes = float(tot.item()) * K
-        pk = torch.tensor([float(n)], dtype=torch.float64, device=dev)
-        dist.all_reduce(pk)
-        job_pkts = float(pk.item()) * K
-    else:
-        job_bytes = float(L_sum) * K
-        job_pkts = float(n) * K
+    elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, float(L_sum) * K, float(n) * K,
+                                                    device=dev if dist else None)
     value = job_bytes / elapsed / GIB
 
     # Roofline of the dominant kernel (k_ipv4_verify).  Algorithmic bytes per

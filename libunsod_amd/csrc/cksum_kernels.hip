@@ -534,19 +534,19 @@ Tuning g_tune = [] {
   return t;
 }();
 
-// Measured on MI355X (tools/sweep.py, profiles/): narrow groups win -- a wave
-// folds 8-16 datagrams at once, so per-packet fixed costs (header broadcast,
-// butterfly, store) are shared and each lane streams several passes.  1500 B:
-// 8x4 / 8x2 = 20.1 us vs 32x3 26 us and 64x4 46 us; 9000 B: every shape is
-// within 1 % of 8x12 (bandwidth-bound).
+// Measured on MI355X (tools/sweep.py, profiles/sweep_r01.jsonl): narrow groups
+// win -- a wave folds 8-16 datagrams at once, so per-packet fixed costs (header
+// broadcast, butterfly, store) are shared and each lane streams several passes.
+// 1500 B: 8x2 20.4 us alone / 14.3 us per launch on 2 streams, vs 32x3 26 us and
+// 64x4 46 us alone; 9000 B: every narrow shape within 1 % of 8x12
+// (bandwidth-bound); 46 B in 64 B slots: 4x2.
 Shape pick_shape(uint32_t max_len) {
   if (g_tune.g) return {g_tune.g, g_tune.u};
   // chunks of the 16-byte envelope, worst-case misalignment
   const uint32_t ch = (max_len + 15u + 15u) / 16u;
-  if (ch <= 4) return {4, 1};
   if (ch <= 8) return {4, 2};
   if (ch <= 16) return {4, 4};
-  if (ch <= 128) return {8, 4};
+  if (ch <= 128) return {8, 2};
   if (ch <= 256) return {8, 8};
   return {8, 12};
 }

@@ -44,3 +44,20 @@ def shard_by_bytes(lengths, world: int, rank: int) -> tuple[int, int]:
 
 def all_shards(lengths, world: int) -> list[tuple[int, int]]:
     return [shard_by_bytes(lengths, world, r) for r in range(world)]
+
+
+def job_totals(elapsed_s: float, nbytes: float, npkts: float, device=None) -> tuple[float, float, float]:
+    """Across the process group (if any): (max elapsed, sum bytes, sum packets).
+
+    The only collective the checksum path uses -- timing bookkeeping, not data.
+    ``device`` is where the reduction tensors live (a CUDA device for nccl/RCCL,
+    None = CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(elapsed_s), float(nbytes), float(npkts)
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([nbytes, npkts], dtype=torch.float64, device=device)
+    dist.all_reduce(s)
+    return float(t.item()), float(s[0].item()), float(s[1].item())
