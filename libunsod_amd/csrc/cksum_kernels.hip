@@ -149,6 +149,7 @@ __device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0
 // group-lane reads of the dwords that cover bytes h .. h+23.
 struct IpHdr {
   uint32_t hl, iplen, proto, src, dst;
+  uint32_t w[5];  // the 20 header bytes as little-endian dwords, stream-aligned
 };
 template <int G>
 __device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
@@ -160,16 +161,23 @@ __device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
     const uint32_t mine = c == 0 ? v0.x : c == 1 ? v0.y : c == 2 ? v0.z : v0.w;
     T[j] = group_lane<G>(mine, idx >> 2);
   }
-  // little-endian u32 at byte h + 4k = alignbyte({T[k+1], T[k]}, rb)
-  const uint32_t w0 = __builtin_amdgcn_alignbyte(T[1], T[0], rb);
-  const uint32_t w2 = __builtin_amdgcn_alignbyte(T[3], T[2], rb);
   IpHdr ih;
-  ih.hl = (w0 & 0x0fu) << 2;
-  ih.iplen = ((w0 >> 8) & 0xff00u) | (w0 >> 24);
-  ih.proto = (w2 >> 8) & 0xffu;
-  ih.src = __builtin_amdgcn_alignbyte(T[4], T[3], rb);
-  ih.dst = __builtin_amdgcn_alignbyte(T[5], T[4], rb);
+  // little-endian u32 at byte h + 4k = alignbyte({T[k+1], T[k]}, rb)
+#pragma unroll
+  for (int k = 0; k < 5; ++k) ih.w[k] = __builtin_amdgcn_alignbyte(T[k + 1], T[k], rb);
+  ih.hl = (ih.w[0] & 0x0fu) << 2;
+  ih.iplen = ((ih.w[0] >> 8) & 0xff00u) | (ih.w[0] >> 24);
+  ih.proto = (ih.w[2] >> 8) & 0xffu;
+  ih.src = ih.w[3];
+  ih.dst = ih.w[4];
   return ih;
+}
+
+// Absolute-lane sum of stream-aligned dwords: even stream bytes go to the low
+// lane unless the datagram starts at an odd address.
+__device__ __forceinline__ uint32_t abs_halves(uint32_t w, bool odd) {
+  const uint32_t e = halves(w & 0x00ff00ffu), o = halves((w >> 8) & 0x00ff00ffu);
+  return odd ? (e << 8) + o : e + (o << 8);
 }
 
 // ------------------------------------------------------------------ kernels
@@ -228,6 +236,13 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
 // Sums of one IPv4 datagram: header [0, hl) and L4 [hl, ip_len) (absolute
 // lanes, unfolded group totals), plus the parsed header.  TX excludes the
 // ip_sum field (bytes 10..11) from the header sum.
+//
+// The chunks fold ONE range, [0, ip_len): a datagram is at most 65535 bytes, so
+// its unfolded 16-bit-lane total is < 2^31 and the L4 sum is that total minus
+// the header sum, exactly (disjoint byte sets, no modular wrap, zero-ness kept).
+// A 20-byte header -- the common case -- is summed from the five dwords the
+// header parse already holds; only datagrams with IP options (hl > 20) fold
+// their header from the chunks.
 template <int G, int U, bool TX>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                           int lane, IpHdr &ih, bool &hdr_ok, bool &l4_ok,
@@ -238,34 +253,43 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   u32x4 v[U];
   issue_pass<G, U>(r, c0, nch, 0, lane, v);
   ih = parse_ipv4<G>(v[0], h);
+  const bool odd = h & 1u;  // base is 16-byte aligned
   hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-  l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-  if (TX) l4_ok = l4_ok && (ih.proto == 6u || ih.proto == 17u);
-  const int hend = hdr_ok && (!TX || (ih.iplen >= ih.hl && ih.iplen <= flen)) ? (int)ih.hl : 0;
+  const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+  l4_ok = TX ? len_ok && (ih.proto == 6u || ih.proto == 17u) : len_ok;
+  const int hend = hdr_ok && (!TX || len_ok) ? (int)ih.hl : 0;
   const int lend = l4_ok ? (int)ih.iplen : hend;
-  uint32_t acc_h = 0, acc_l = 0;
+  const bool opts = hend > 20;  // group-uniform
+  uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
   for (uint32_t p = 0;;) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
-      const bool pure = rel >= hend && rel + 16 <= lend;
-      acc_l += pure ? sum4(v[u]) : 0u;
-      if (!pure && rel < lend) {
-        if (TX) {
-          // ip_sum is zeroed before in_cksum (ip_output.c:670-672)
-          acc_h += range_sum(v[u], rel, 0, min(hend, 10)) + range_sum(v[u], rel, 12, hend);
-        } else {
-          acc_h += range_sum(v[u], rel, 0, hend);
-        }
-        acc_l += range_sum(v[u], rel, hend, lend);
+      const bool pure = rel >= 0 && rel + 16 <= lend;
+      acc_t += pure ? sum4(v[u]) : 0u;
+      if (!pure && rel < lend) acc_t += range_sum(v[u], rel, 0, lend);
+      if (opts && rel < hend) {
+        acc_h += range_sum(v[u], rel, 0, hend);
+        if (TX) acc_f += range_sum(v[u], rel, 10, 12);
       }
     }
-    acc_l = fold16(acc_l);
     if (++p >= npass) break;
     issue_pass<G, U>(r, c0, nch, p, lane, v);
   }
-  sum_h = group_sum<G>(fold16(acc_h));
-  sum_l = group_sum<G>(acc_l);
+  const uint32_t total = group_sum<G>(acc_t);
+  uint32_t hdr, field;
+  if (opts) {
+    hdr = group_sum<G>(acc_h);
+    field = TX ? group_sum<G>(acc_f) : 0u;
+  } else if (hend) {
+    hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+          abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+    field = TX ? abs_halves(ih.w[2] & 0xffff0000u, odd) : 0u;
+  } else {
+    hdr = field = 0u;
+  }
+  sum_h = hdr - field;  // TX: ip_sum is zeroed before in_cksum (ip_output.c:670-672)
+  sum_l = total - hdr;
 }
 
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
