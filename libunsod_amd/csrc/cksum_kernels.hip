@@ -245,13 +245,11 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
 // their header from the chunks.
 template <int G, int U, bool TX>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
-                                          int lane, IpHdr &ih, bool &hdr_ok, bool &l4_ok,
-                                          uint32_t &sum_h, uint32_t &sum_l) {
+                                          int lane, u32x4 (&v)[U], IpHdr &ih, bool &hdr_ok,
+                                          bool &l4_ok, uint32_t &sum_h, uint32_t &sum_l) {
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = (h + flen + 15u) >> 4;
   const uint32_t npass = (nch + G * U - 1) / (G * U);
-  u32x4 v[U];
-  issue_pass<G, U>(r, c0, nch, 0, lane, v);
   ih = parse_ipv4<G>(v[0], h);
   const bool odd = h & 1u;  // base is 16-byte aligned
   hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
@@ -292,6 +290,55 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   sum_l = total - hdr;
 }
 
+// Grid-stride walk over the packets of a batch, one packet per lane group at a
+// time, with the FIRST pass of the group's next packet issued before the
+// current packet is folded: a group keeps two packets' loads in flight, which
+// is what small datagrams (one pass each) need to cover HBM latency.
+template <int G, int U>
+__device__ __forceinline__ void issue_first(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
+                                            int lane, u32x4 (&v)[U]) {
+  issue_pass<G, U>(r, off & ~15u, flen ? ((off & 15u) + flen + 15u) >> 4 : 0u, 0, lane, v);
+}
+
+template <int G, int U, typename Body>
+__device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_rsrc_t r, int lane,
+                                                Body body) {
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  if (i >= d.n) return;
+  if constexpr (U > 4) {
+    // wide shapes already keep U loads per lane in flight; double-buffering
+    // them would cost occupancy (8x12: 121 -> 172 VGPRs)
+    for (; i < d.n; i += stride) {
+      const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+      u32x4 v[U];
+      issue_first<G, U>(r, off, flen, lane, v);
+      body(i, off, flen, v);
+    }
+    return;
+  }
+  uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+  u32x4 v[U];
+  issue_first<G, U>(r, off, flen, lane, v);
+  for (;;) {
+    const uint32_t in = i + stride;
+    const bool more = in < d.n;
+    uint32_t offn = 0, flenn = 0;
+    if (more) {
+      offn = pkt_off(d, in);
+      flenn = pkt_len(d, in);
+    }
+    u32x4 vn[U];
+    issue_first<G, U>(r, offn, flenn, lane, vn);
+    body(i, off, flen, v);
+    if (!more) break;
+    i = in;
+    off = offn;
+    flen = flenn;
+    for (int u = 0; u < U; ++u) v[u] = vn[u];
+  }
+}
+
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
@@ -299,13 +346,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
                                                         uint32_t *bad) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
-  const uint32_t stride = gridDim.x * (kBlock / G);
-  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
-    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+  for_each_packet<G, U>(d, r, lane, [&](uint32_t i, uint32_t off, uint32_t flen, u32x4 (&v)[U]) {
     IpHdr ih;
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, U, false>(r, off, flen, lane, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
       uint32_t ip = 0, l4 = 0, st = 0;
@@ -331,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
       if (st_out) st_out[i] = (uint8_t)st;
       if (bad && st) atomicAdd(bad, 1u);
     }
-  }
+  });
 }
 
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
@@ -340,13 +385,11 @@ template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
-  const uint32_t stride = gridDim.x * (kBlock / G);
-  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < d.n; i += stride) {
-    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+  for_each_packet<G, U>(d, r, lane, [&](uint32_t i, uint32_t off, uint32_t flen, u32x4 (&v)[U]) {
     IpHdr ih;
     bool hdr_ok, do_l4;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, U, true>(r, off, flen, lane, ih, hdr_ok, do_l4, sum_h, sum_l);
+    ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l);
     const bool ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
     if (lane == 0 && ok) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
@@ -367,7 +410,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + 11u, 0, 0);
     }
-  }
+  });
 }
 
 // ---------------------------------------------------------- workload generator
