@@ -151,15 +151,26 @@ struct IpHdr {
   uint32_t hl, iplen, proto, src, dst;
   uint32_t w[5];  // the 20 header bytes as little-endian dwords, stream-aligned
 };
-template <int G>
-__device__ __forceinline__ IpHdr parse_ipv4(const u32x4 &v0, uint32_t h) {
+template <int G, int U>
+__device__ __forceinline__ IpHdr parse_ipv4(const u32x4 (&v)[U], uint32_t h) {
   const uint32_t q = h >> 2, rb = h & 3u;
   uint32_t T[6];
+  if constexpr (G == 1) {
+    // lane-per-packet: chunks 0..2 are this lane's v[0..2]
+    static_assert(U >= 3, "a lone lane needs the 35-byte header window in one pass");
+    const uint32_t D[12] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y,
+                            v[1].z, v[1].w, v[2].x, v[2].y, v[2].z, v[2].w};
 #pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const uint32_t idx = q + j, c = idx & 3u;
-    const uint32_t mine = c == 0 ? v0.x : c == 1 ? v0.y : c == 2 ? v0.z : v0.w;
-    T[j] = group_lane<G>(mine, idx >> 2);
+    for (int j = 0; j < 6; ++j)
+      T[j] = q == 0 ? D[j] : q == 1 ? D[j + 1] : q == 2 ? D[j + 2] : D[j + 3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const uint32_t idx = q + j, c = idx & 3u;
+      const u32x4 &v0 = v[0];
+      const uint32_t mine = c == 0 ? v0.x : c == 1 ? v0.y : c == 2 ? v0.z : v0.w;
+      T[j] = group_lane<G>(mine, idx >> 2);
+    }
   }
   IpHdr ih;
   // little-endian u32 at byte h + 4k = alignbyte({T[k+1], T[k]}, rb)
@@ -250,7 +261,7 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = (h + flen + 15u) >> 4;
   const uint32_t npass = (nch + G * U - 1) / (G * U);
-  ih = parse_ipv4<G>(v[0], h);
+  ih = parse_ipv4<G, U>(v, h);
   const bool odd = h & 1u;  // base is 16-byte aligned
   hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
   const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
@@ -573,7 +584,7 @@ int ensure_ctx() {
 // the shape only sets how many bytes a wave keeps in flight and how many slots
 // go unused.  FOR_GU lists the instantiated shapes.
 #define FOR_GU(X)                                                                  \
-  X(4, 1) X(4, 2) X(4, 4) X(8, 2) X(8, 4) X(8, 8) X(8, 12) X(16, 2) X(16, 4)       \
+  X(1, 4) X(1, 8) X(4, 1) X(4, 2) X(4, 4) X(8, 2) X(8, 4) X(8, 8) X(8, 12) X(16, 2) X(16, 4)       \
   X(16, 6) X(16, 8) X(32, 2) X(32, 3) X(32, 4) X(32, 6) X(64, 2) X(64, 3) X(64, 4) \
   X(64, 6) X(64, 9)
 
@@ -611,6 +622,7 @@ Shape pick_shape(uint32_t max_len) {
   if (g_tune.g) return {g_tune.g, g_tune.u};
   // chunks of the 16-byte envelope, worst-case misalignment
   const uint32_t ch = (max_len + 15u + 15u) / 16u;
+  if (ch <= 4) return {1, 4};
   if (ch <= 8) return {4, 2};
   if (ch <= 16) return {4, 4};
   if (ch <= 128) return {8, 2};

@@ -248,3 +248,35 @@ def test_deterministic_and_stream_async():
     assert mi.ipv4_verify_repeat([b], outs, 6, nstreams=3, timing="region") > 0
     for k in ("ip", "l4", "status"):
         assert np.array_equal(cpu(outs[0][k]), cpu(r1[k]))
+
+
+SHAPES = [(1, 4), (1, 8), (4, 1), (4, 2), (4, 4), (8, 2), (8, 4), (8, 8), (8, 12), (16, 2), (16, 4), (16, 6),
+          (16, 8), (32, 2), (32, 3), (32, 4), (32, 6), (64, 2), (64, 3), (64, 4), (64, 6), (64, 9)]
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_every_shape_bit_exact(golden, shape):
+    """The lane-group shape (and grid cap) changes speed only: every compiled
+    shape reproduces the reference's verify / finalize / span results."""
+    g = golden
+    n = len(g["vb_offs"])
+    offs = dev_tensor(g["vb_offs"].astype(np.int64))
+    lens = dev_tensor(g["vb_flen"].astype(np.int32))
+    mi.set_shape(shape[0], shape[1], 97)  # odd grid cap: many packets per group
+    try:
+        buf = dev_tensor(g["ver_in"])
+        r = mi.ipv4_verify(mi.PktBatch(buf, n, offs=offs, lens=lens))
+        assert np.array_equal(cpu(r["ip"]), g["ver_ip"])
+        assert np.array_equal(cpu(r["l4"]), g["ver_l4"])
+        assert np.array_equal(cpu(r["status"]), g["ver_st"])
+        fin = dev_tensor(g["fin_in"])
+        mi.ipv4_finalize(mi.PktBatch(fin, n, offs=offs, lens=lens))
+        assert np.array_equal(cpu(fin), g["fin_out"])
+        # spans: in_cksum_skip over every datagram region of the verify buffer
+        sp = cpu(mi.span_batch(mi.PktBatch(buf, n, offs=offs, lens=lens)))
+        _, h = aligned(g["ver_in"])
+        for i in range(0, n, 7):
+            o, L = int(g["vb_offs"][i]), int(g["vb_flen"][i])
+            assert sp[i] == ORC.chain_skip([(h[o:o + L].tobytes(), o % 64)], L, 0)
+    finally:
+        mi.set_shape(0, 0, 0)

@@ -23,7 +23,7 @@ import torch  # noqa: E402
 import libunsod_amd as mi  # noqa: E402
 from libunsod_amd import synth  # noqa: E402
 
-SHAPES = [(4, 1), (4, 2), (4, 4), (8, 2), (8, 4), (8, 8), (8, 12), (16, 2), (16, 4), (16, 6), (16, 8), (32, 2),
+SHAPES = [(1, 4), (1, 8), (4, 1), (4, 2), (4, 4), (8, 2), (8, 4), (8, 8), (8, 12), (16, 2), (16, 4), (16, 6), (16, 8), (32, 2),
           (32, 3), (32, 4), (32, 6), (64, 2), (64, 3), (64, 4), (64, 6), (64, 9)]
 CONFIGS = {"1500": (65536, 1500, 2176, 142), "9000": (65536, 9000, 9216, 142), "64": (1 << 20, 46, 64, 14)}
 
