@@ -181,23 +181,30 @@ def main():
     }
 
     # -------------------------------------------- CPU baseline + host path
-    if world == 1 and rank == 0 and args.config != "pareto":
+    if world == 1 and rank == 0:
         host = batches[0].buf.cpu().numpy()
+        lay = dict(stride=stride, first_off=first, fixed_len=L) if lens is None else dict(offs=offs, lens=lens)
         if args.cpu_seconds > 0:
-            result["cpu_baseline"] = cpu_baseline(host, n, L, stride, first, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(host, n, L_sum, lay, args.cpu_seconds)
         if not args.no_host_path:
-            result["pcie_inclusive"] = host_path(mi, host, n, L, stride, first)
+            result["pcie_inclusive"] = host_path(mi, host, n, L_sum, lay)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(host: np.ndarray, n: int, L: int, stride: int, first: int, seconds: float) -> dict:
+def _oracle_layout(lay: dict) -> dict:
+    if "offs" in lay:
+        return dict(offs=lay["offs"], flen=lay["lens"].astype(np.uint32))
+    return dict(stride=lay["stride"], first_off=lay["first_off"], fixed_flen=lay["fixed_len"])
+
+
+def cpu_baseline(host: np.ndarray, n: int, L_sum: int, lay: dict, seconds: float) -> dict:
     """The reference CPU path on the same bytes: ipv4_verify_batch drives
     in_cksum_hdr + in_cksum_pseudo_header per packet exactly as ip_input /
-    tcp_input call them.  1 thread, repeated passes over (a prefix of) the batch
-    until `seconds` of CPU work."""
+    tcp_input call them.  1 thread, repeated passes over the batch until
+    `seconds` of CPU work."""
     from oracle.pyoracle import Oracle, available
     kind = "reference" if available("reference") else "port"
     o = Oracle(kind)
@@ -205,23 +212,25 @@ def cpu_baseline(host: np.ndarray, n: int, L: int, stride: int, first: int, seco
     s = (-raw.ctypes.data) % 64
     h = raw[s:s + host.size]
     h[:] = host
-    ip, l4, st = o.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+    ol = _oracle_layout(lay)
+    ip, l4, st = o.ipv4_verify_batch(h, n, **ol)
     assert not st.any(), "CPU baseline disagrees: batch should verify"
     passes, t0 = 0, time.perf_counter()
     while True:
-        o.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+        o.ipv4_verify_batch(h, n, **ol)
         passes += 1
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return dict(value=round(passes * n * L / dt / GIB, 3), unit="GiB/s", cores=1, kind=kind,
-                sample=f"{passes} passes x {n} x {L} B datagrams ({dt:.1f} s, 1 thread): in_cksum_hdr + "
-                       f"in_cksum_pseudo_header per packet, {'oracle/_ref (reference in_cksum.c)' if kind == 'reference' else 'oracle restatement'}, "
+    src = "oracle/_ref (reference in_cksum.c)" if kind == "reference" else "oracle restatement"
+    return dict(value=round(passes * L_sum / dt / GIB, 3), unit="GiB/s", cores=1, kind=kind,
+                sample=f"{passes} passes x {n} datagrams, {L_sum} B each pass ({dt:.1f} s, 1 thread): "
+                       f"in_cksum_hdr + in_cksum_pseudo_header per packet, {src}, "
                        f"gcc -O3 -frename-registers -fno-strict-aliasing",
                 cpu=_cpu_model())
 
 
-def host_path(mi, host: np.ndarray, n: int, L: int, stride: int, first: int, iters: int = 5) -> dict:
+def host_path(mi, host: np.ndarray, n: int, L_sum: int, lay: dict, iters: int = 5) -> dict:
     """PCIe-inclusive rate: the batch starts and ends in (page-locked) host
     memory; chunked H2D -> verify -> D2H (mi_cksum_ipv4_verify_host)."""
     pinned = True
@@ -229,16 +238,16 @@ def host_path(mi, host: np.ndarray, n: int, L: int, stride: int, first: int, ite
         mi.host_register(host)
     except Exception:
         pinned = False
-    mi.ipv4_verify_host(host, n, stride=stride, first_off=first, fixed_len=L)
+    mi.ipv4_verify_host(host, n, **lay)
     t0 = time.perf_counter()
     for _ in range(iters):
-        _, _, st, bad = mi.ipv4_verify_host(host, n, stride=stride, first_off=first, fixed_len=L)
+        _, _, st, bad = mi.ipv4_verify_host(host, n, **lay)
     dt = (time.perf_counter() - t0) / iters
     if pinned:
         mi.host_unregister(host)
     assert bad == 0
-    return dict(value=round(n * L / dt / GIB, 2), unit="GiB/s", pinned=pinned,
-                bytes_moved_per_batch=int(host.nbytes), ms_per_batch=round(dt * 1e3, 3))
+    return dict(value=round(L_sum / dt / GIB, 2), unit="GiB/s", pinned=pinned,
+                host_buffer_bytes=int(host.nbytes), ms_per_batch=round(dt * 1e3, 3))
 
 
 def _cpu_model() -> str:

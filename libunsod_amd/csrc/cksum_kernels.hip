@@ -612,26 +612,28 @@ Tuning g_tune = [] {
   return t;
 }();
 
-// Measured on MI355X (tools/sweep.py, profiles/sweep_r01.jsonl): narrow groups
-// win -- a wave folds 8-16 datagrams at once, so per-packet fixed costs (header
-// broadcast, butterfly, store) are shared and each lane streams several passes.
-// 1500 B: 8x2 20.4 us alone / 14.3 us per launch on 2 streams, vs 32x3 26 us and
-// 64x4 46 us alone; 9000 B: every narrow shape within 1 % of 8x12
-// (bandwidth-bound); 46 B in 64 B slots: 4x2.
+// Measured on MI355X (tools/sweep.py, profiles/sweep_r01*.jsonl): narrow groups
+// win -- a wave folds 4-64 datagrams at once, so per-packet fixed costs (header
+// broadcast, butterfly, store) are shared and each lane streams several
+// chunks.  GPU time per launch on 2 streams: 1500 B 16x6 14.0 us (8x2 14.3,
+// 32x3 and 64x4 far behind even alone: 26 / 46 us); 9000 B every narrow shape
+// within 1 % of 8x12 (bandwidth-bound); 46 B datagrams in 64 B slots: one lane
+// per packet, 1x4 19.2 us vs 4x2 26.2 us.
 Shape pick_shape(uint32_t max_len) {
   if (g_tune.g) return {g_tune.g, g_tune.u};
   // chunks of the 16-byte envelope, worst-case misalignment
   const uint32_t ch = (max_len + 15u + 15u) / 16u;
   if (ch <= 4) return {1, 4};
-  if (ch <= 8) return {4, 2};
+  if (ch <= 8) return {1, 8};
   if (ch <= 16) return {4, 4};
-  if (ch <= 128) return {8, 2};
+  if (ch <= 48) return {8, 4};
+  if (ch <= 128) return {16, 6};
   if (ch <= 256) return {8, 8};
   return {8, 12};
 }
 
 int grid_for(uint32_t n, int G) {
-  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 4096;
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 2048;
   const uint64_t groups_per_block = kBlock / G;
   uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
   if (blocks > (uint64_t)cap) blocks = cap;
@@ -961,6 +963,13 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
   HIP_TRY(hipStreamSynchronize(c.hstream[0]));
 
   const Shape G = pick_shape(max_len);
+  // fixed slots whose envelope is narrower than the slot: pitched copy
+  static const bool allow_2d = [] {
+    const char *e = getenv("MI_CKSUM_HOST_2D");
+    return !(e && e[0] == '0');
+  }();
+  const uint64_t env_w = ((b->first_off & 15u) + b->fixed_len + 15u) & ~15ull;
+  const bool pitched = allow_2d && !var && b->stride % 16 == 0 && env_w + 64 <= b->stride;
   bool used[ThreadCtx::kRing] = {};
   int k = 0;
   for (uint32_t i = 0; i < b->n;) {
@@ -989,7 +998,16 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
       d.stride = b->stride;
       d.fixed_len = b->fixed_len;
     }
-    HIP_TRY(hipMemcpyAsync(c.dstage[k], hb + s0, end - s0, hipMemcpyHostToDevice, st));
+    if (pitched) {
+      // only the 16-byte envelopes cross PCIe: one rectangular DMA, source
+      // pitch = slot stride, destination pitch = envelope (slot gaps stay home)
+      HIP_TRY(hipMemcpy2DAsync(c.dstage[k], env_w, hb + s0, b->stride, env_w, d.n,
+                               hipMemcpyHostToDevice, st));
+      d.stride = env_w;
+      d.bytes = (uint32_t)(env_w * d.n);
+    } else {
+      HIP_TRY(hipMemcpyAsync(c.dstage[k], hb + s0, end - s0, hipMemcpyHostToDevice, st));
+    }
     uint16_t *dip = c.dout[k], *dl4 = c.dout[k] + max_pk;
     rc = launch_verify(d, G, ip_sum ? dip : nullptr, l4_sum ? dl4 : nullptr,
                        status ? c.dst8[k] : nullptr, c.dbad + k, st);
