@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--grids", default="0,1024,2048,8192,16384")
     ap.add_argument("--streams", default="1,2,3,4")
+    ap.add_argument("--shapes", default="", help="e.g. 8x2,16x6 (default: all that fit)")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved repetitions of the whole grid")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     for cfg in a.configs.split(","):
@@ -70,8 +72,9 @@ def main():
                      status=torch.empty(n, dtype=torch.uint8, device=dev)) for _ in bs]
         torch.cuda.synchronize()
         ch = (maxlen + 30) // 16
-        for g, u in SHAPES:
-            if g * u > 4 * max(ch, 4) or g * u * 9 < ch:  # skip hopeless shapes
+        shapes = [tuple(int(x) for x in t.split("x")) for t in a.shapes.split(",")] if a.shapes else SHAPES
+        for rnd, (g, u) in [(r, sh) for r in range(a.rounds) for sh in shapes]:
+            if not a.shapes and (g * u > 4 * max(ch, 4) or g * u * 9 < ch):  # skip hopeless shapes
                 continue
             for grid in [int(x) for x in a.grids.split(",")]:
                 mi.set_shape(g, u, grid)
@@ -86,7 +89,7 @@ def main():
                     torch.cuda.synchronize()
                     ok = int(chk["bad"].item()) == 0
                     med = float(np.median(iso))
-                    print(json.dumps(dict(config=cfg, g=g, u=u, grid=grid, streams=ns, iso_kern_us=round(med, 2),
+                    print(json.dumps(dict(config=cfg, round=rnd, g=g, u=u, grid=grid, streams=ns, iso_kern_us=round(med, 2),
                                           iso_GBps=round((lsum + 5 * n) / med / 1e3, 1),
                                           gpu_us_per_launch=round(span / a.steps, 2),
                                           step_us=round(dt / a.steps * 1e6, 2),
