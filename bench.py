@@ -69,12 +69,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # MI_BENCH_DEVICE / MI_BENCH_BACKEND exist only to rehearse the N>1 path on
+    # a one-GPU box (all ranks on one device, gloo); the driver's runs use
+    # LOCAL_RANK and RCCL ("nccl").
+    gpu = int(os.environ.get("MI_BENCH_DEVICE", local))
+    backend = os.environ.get("MI_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import libunsod_amd as mi
     from libunsod_amd import shard, synth
@@ -132,7 +140,7 @@ def main():
         mi.ipv4_verify_repeat(batches, outs, args.warmup, nstreams=nst, timing="none")
     torch.cuda.synchronize()
     # Settle: the first ~0.1 s of back-to-back launches run up to 20 % slower
-    # (clock / translation warm-up; profiles/warmup_r01.json: 40 warmup steps ->
+    # (clock / translation warm-up; profiles/warmup_r01.jsonl: 40 warmup steps ->
     # 17.0 us per launch, 2000 -> 14.25 us).  Keep launching untimed steps until
     # the warmup phase has lasted `--settle` seconds, whatever W is.
     settle_steps = 0
@@ -156,7 +164,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, float(L_sum) * K, float(n) * K,
-                                                    device=dev if dist else None)
+                                                    device=dev if dist and backend == "nccl" else None)
     value = job_bytes / elapsed / GIB
 
     # Roofline of the dominant kernel (k_ipv4_verify).  Algorithmic bytes per

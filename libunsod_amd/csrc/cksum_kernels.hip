@@ -112,6 +112,7 @@ struct Desc {
   uint64_t stride, first_off;
   const uint32_t *lens;
   uint32_t fixed_len;
+  uint32_t len_lo, len_hi;  // length class filter: only lo <= lens[i] < hi (lens != NULL)
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
@@ -315,12 +316,23 @@ template <int G, int U, typename Body>
 __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_rsrc_t r, int lane,
                                                 Body body) {
   const uint32_t stride = gridDim.x * (kBlock / G);
-  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  const bool filter = d.lens && (d.len_lo != 0u || d.len_hi != ~0u);  // launch-uniform
+  // next packet index >= i of this launch's length class (group-uniform walk)
+  auto next = [&](uint32_t i) {
+    if (filter)
+      while (i < d.n) {
+        const uint32_t l = d.lens[i];
+        if (l >= d.len_lo && l < d.len_hi) break;
+        i += stride;
+      }
+    return i;
+  };
+  uint32_t i = next(blockIdx.x * (kBlock / G) + threadIdx.x / G);
   if (i >= d.n) return;
   if constexpr (U > 4) {
     // wide shapes already keep U loads per lane in flight; double-buffering
     // them would cost occupancy (8x12: 121 -> 172 VGPRs)
-    for (; i < d.n; i += stride) {
+    for (; i < d.n; i = next(i + stride)) {
       const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
       u32x4 v[U];
       issue_first<G, U>(r, off, flen, lane, v);
@@ -332,7 +344,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
   u32x4 v[U];
   issue_first<G, U>(r, off, flen, lane, v);
   for (;;) {
-    const uint32_t in = i + stride;
+    const uint32_t in = next(i + stride);
     const bool more = in < d.n;
     uint32_t offn = 0, flenn = 0;
     if (more) {
@@ -482,6 +494,7 @@ __global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t byt
                                                uint32_t src, uint32_t dst, uint32_t proto,
                                                uint32_t plen, uint16_t *out) {
   Desc d{};
+  d.len_hi = ~0u;
   d.base = base; d.bytes = bytes; d.n = 1; d.first_off = off; d.fixed_len = len;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   constexpr int G = 64;
@@ -659,6 +672,8 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
   d->first_off = b->first_off;
   d->lens = b->lens;
   d->fixed_len = b->fixed_len;
+  d->len_lo = 0;
+  d->len_hi = ~0u;
   return 0;
 }
 
@@ -672,8 +687,8 @@ int launched() {
   return 0;
 }
 
-int launch_verify(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad,
-                  hipStream_t s) {
+int launch_verify_shape(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uint8_t *st,
+                        uint32_t *bad, hipStream_t s) {
   const int grid = grid_for(d.n, sh.g);
 #define X(G_, U_)                                                                        \
   if (sh.g == G_ && sh.u == U_) {                                                        \
@@ -684,6 +699,29 @@ int launch_verify(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uint8_t *
   FOR_GU(X)
 #undef X
   return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
+}
+
+// Mixed lengths (per-packet lens, long tail): one launch per length class, each
+// with the shape that class wants, so the groups of a wave finish together
+// (a 9000 B datagram no longer holds up a wave of 100 B ones).  Class edges sit
+// on pick_shape's boundaries.  The classes only partition the packets; every
+// packet is folded exactly once.
+constexpr uint32_t kClassEdges[] = {0u, 99u, 739u, 2019u, ~0u};
+
+int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
+                  uint32_t *bad, hipStream_t s) {
+  if (!d.lens || g_tune.g || max_len < kClassEdges[1])
+    return launch_verify_shape(d, pick_shape(max_len), ip, l4, st, bad, s);
+  for (int c = 0; c + 1 < (int)(sizeof kClassEdges / sizeof kClassEdges[0]); ++c) {
+    if (kClassEdges[c] > max_len) break;
+    Desc dc = d;
+    dc.len_lo = kClassEdges[c];
+    dc.len_hi = kClassEdges[c + 1];
+    const uint32_t top = dc.len_hi == ~0u ? max_len : min(max_len, dc.len_hi - 1);
+    int rc = launch_verify_shape(dc, pick_shape(top), ip, l4, st, bad, s);
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd, uint16_t *out,
@@ -767,7 +805,7 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (rc) return rc;
   if ((rc = make_desc(b, &d))) return rc;
   if (!d.n) return 0;
-  return launch_verify(d, pick_shape(batch_max_len(b)), ip_sum, l4_sum, status, bad_count,
+  return launch_verify(d, batch_max_len(b), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
 }
 
@@ -783,10 +821,10 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
   if (timing == MI_TIME_PER_PASS && !kernel_us) return set_err(-EINVAL, "kernel_us is NULL");
   ThreadCtx &c = t_ctx;
   Desc d[16];
-  Shape G[16];
+  uint32_t ml[16];
   for (uint32_t k = 0; k < nb; ++k) {
     if ((rc = make_desc(&b[k], &d[k]))) return rc;
-    G[k] = pick_shape(batch_max_len(&b[k]));
+    ml[k] = batch_max_len(&b[k]);
   }
   // library-owned non-blocking streams: never implicitly serialised against
   // each other or against the legacy default stream
@@ -816,7 +854,7 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
     const uint32_t j = k % nb;
     hipStream_t st = c.rstream[k % nstreams];
     if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k], st));
-    if ((rc = launch_verify(d[j], G[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
+    if ((rc = launch_verify(d[j], ml[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
                             status ? status[j] : nullptr, nullptr, st)))
       return rc;
     if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k + 1], st));
@@ -962,7 +1000,6 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
   HIP_TRY(hipMemsetAsync(c.dbad, 0, 4 * ThreadCtx::kRing, c.hstream[0]));
   HIP_TRY(hipStreamSynchronize(c.hstream[0]));
 
-  const Shape G = pick_shape(max_len);
   // fixed slots whose envelope is narrower than the slot: pitched copy
   static const bool allow_2d = [] {
     const char *e = getenv("MI_CKSUM_HOST_2D");
@@ -977,6 +1014,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
     const uint32_t j = chunk_end(i, &s0, &end);
     hipStream_t st = c.hstream[k];
     Desc d{};
+    d.len_hi = ~0u;
     d.base = c.dstage[k];
     d.bytes = (uint32_t)((end - s0 + 15u) & ~15ull);
     d.n = j - i;
@@ -1009,7 +1047,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
       HIP_TRY(hipMemcpyAsync(c.dstage[k], hb + s0, end - s0, hipMemcpyHostToDevice, st));
     }
     uint16_t *dip = c.dout[k], *dl4 = c.dout[k] + max_pk;
-    rc = launch_verify(d, G, ip_sum ? dip : nullptr, l4_sum ? dl4 : nullptr,
+    rc = launch_verify(d, max_len, ip_sum ? dip : nullptr, l4_sum ? dl4 : nullptr,
                        status ? c.dst8[k] : nullptr, c.dbad + k, st);
     if (rc) return rc;
     if (ip_sum) HIP_TRY(hipMemcpyAsync(ip_sum + i, dip, 2ull * d.n, hipMemcpyDeviceToHost, st));
