@@ -315,24 +315,45 @@ __device__ __forceinline__ void issue_first(__amdgpu_buffer_rsrc_t r, uint32_t o
 template <int G, int U, typename Body>
 __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_rsrc_t r, int lane,
                                                 Body body) {
-  const uint32_t stride = gridDim.x * (kBlock / G);
-  const bool filter = d.lens && (d.len_lo != 0u || d.len_hi != ~0u);  // launch-uniform
-  // next packet index >= i of this launch's length class (group-uniform walk)
-  auto next = [&](uint32_t i) {
-    if (filter)
-      while (i < d.n) {
-        const uint32_t l = d.lens[i];
-        if (l >= d.len_lo && l < d.len_hi) break;
-        i += stride;
+  if (d.lens && (d.len_lo != 0u || d.len_hi != ~0u)) {
+    // Length-class launch: each wave scans windows of 64 packets with one
+    // coalesced load of lens[], ballots the members of this launch's class,
+    // compacts their indices through 64 words of LDS, and hands them to its
+    // groups round-robin.  Rare classes cost one load per 64 packets.
+    __shared__ uint32_t sel[kBlock];
+    const uint32_t lane64 = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint32_t gpw = 64u / G, gid = lane64 / G;  // groups per wave, group id in wave
+    const uint32_t nwaves = gridDim.x * (kBlock / 64);
+    for (uint32_t base = (blockIdx.x * (kBlock / 64) + wv) * 64u; base < d.n; base += nwaves * 64u) {
+      const uint32_t k = base + lane64;
+      const uint32_t l = k < d.n ? d.lens[k] : 0u;
+      const bool in = k < d.n && l >= d.len_lo && l < d.len_hi;
+      const uint64_t m = __ballot(in);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (in) sel[wv * 64u + below] = k;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t cnt = __popcll(m);
+      for (uint32_t q = gid; q < cnt; q += gpw) {
+        const uint32_t i = sel[wv * 64u + q];
+        const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+        u32x4 v[U];
+        issue_first<G, U>(r, off, flen, lane, v);
+        body(i, off, flen, v);
       }
-    return i;
-  };
-  uint32_t i = next(blockIdx.x * (kBlock / G) + threadIdx.x / G);
+      __builtin_amdgcn_wave_barrier();  // sel[] is rewritten by the next window
+    }
+    return;
+  }
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
   if (i >= d.n) return;
   if constexpr (U > 4) {
     // wide shapes already keep U loads per lane in flight; double-buffering
     // them would cost occupancy (8x12: 121 -> 172 VGPRs)
-    for (; i < d.n; i = next(i + stride)) {
+    for (; i < d.n; i += stride) {
       const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
       u32x4 v[U];
       issue_first<G, U>(r, off, flen, lane, v);
@@ -344,7 +365,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
   u32x4 v[U];
   issue_first<G, U>(r, off, flen, lane, v);
   for (;;) {
-    const uint32_t in = next(i + stride);
+    const uint32_t in = i + stride;
     const bool more = in < d.n;
     uint32_t offn = 0, flenn = 0;
     if (more) {
