@@ -120,7 +120,8 @@ def main():
             b = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
         else:
             b = mi.PktBatch(buf, n, offs=torch.from_numpy(offs.astype(np.int64)).to(dev),
-                            lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()))
+                            lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()),
+                            packed=True)
         mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r + 104729 * rank)
         mi.ipv4_finalize(b)  # TX path makes every packet valid
         batches.append(b)

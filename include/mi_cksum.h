@@ -94,6 +94,11 @@ int mi_cksum_set_shape(int group, int chunks, int max_blocks);
  *   Packet i starts at base + (offs ? offs[i] : first_off + i * stride) and is
  *   lens[i] (or fixed_len) bytes long.  offs / lens are device arrays.
  *   max_len   upper bound of lens[] (0 = unknown); sizes the lane groups.
+ *   flags     MI_BATCH_PACKED: a hint that offs[] ascend and the datagrams sit
+ *             back to back (gaps < 64 B), e.g. a mixed-length batch packed at
+ *             8-byte offsets; verify then streams each 64-datagram range as one
+ *             flat run.  Ranges that turn out not packed are still verified
+ *             correctly (per-datagram fallback), only slower.
  * Spans outside [0, bytes) read as zero bytes (hardware bounds check), never
  * fault.
  */
@@ -107,8 +112,10 @@ typedef struct mi_pkt_batch {
 	uint32_t        fixed_len;
 	uint32_t        n;
 	uint32_t        max_len;
-	uint32_t        reserved;
+	uint32_t        flags;
 } mi_pkt_batch;
+
+#define MI_BATCH_PACKED 1u
 
 /* Lane conventions for mi_cksum_span_batch. */
 #define MI_SPAN_STREAM 0u  /* in_cksum_skip / in_cksum_pseudo_header: lanes

@@ -18,6 +18,7 @@ MI_SPAN_ABS = 1
 MI_ST_IP_BAD = 1
 MI_ST_L4_BAD = 2
 MI_ST_MALFORMED = 4
+MI_BATCH_PACKED = 1
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2
@@ -43,7 +44,7 @@ class PktBatchC(C.Structure):
         ("fixed_len", C.c_uint32),
         ("n", C.c_uint32),
         ("max_len", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("flags", C.c_uint32),
     ]
 
 

@@ -113,6 +113,7 @@ struct Desc {
   const uint32_t *lens;
   uint32_t fixed_len;
   uint32_t len_lo, len_hi;  // length class filter: only lo <= lens[i] < hi (lens != NULL)
+  uint32_t flags;           // MI_BATCH_*
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
@@ -383,6 +384,36 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
   }
 }
 
+// RX verify outputs of one datagram from its absolute-lane header / L4 sums
+// (ip_input.c:459-471, tcp_input.c:697-720).
+__device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok,
+                                             bool l4_ok, uint32_t sum_h, uint32_t sum_l,
+                                             uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                             uint32_t *bad) {
+  uint32_t ip = 0, l4 = 0, st = 0;
+  if (!hdr_ok) {
+    st = MI_ST_MALFORMED;
+  } else {
+    uint32_t sh = fold16(sum_h);
+    if (ih.hl != 20u && odd) sh = swap16(sh);  // in_cksum (stream) vs in_cksum_hdr (abs)
+    ip = ~sh & 0xffffu;
+    if (l4_ok) {
+      uint32_t sl = fold16(sum_l);
+      if (odd) sl = swap16(sl);
+      const uint32_t plen = ih.iplen - ih.hl;
+      const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(plen);
+      l4 = ~fold16_64(seed + sl) & 0xffffu;
+    } else {
+      st = MI_ST_MALFORMED;
+    }
+    st |= (ip ? MI_ST_IP_BAD : 0u) | (l4 ? MI_ST_L4_BAD : 0u);
+  }
+  if (ip_out) ip_out[i] = (uint16_t)ip;
+  if (l4_out) l4_out[i] = (uint16_t)l4;
+  if (st_out) st_out[i] = (uint8_t)st;
+  if (bad && st) atomicAdd(bad, 1u);
+}
+
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
@@ -395,32 +426,124 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
     ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
-    if (lane == 0) {
-      const bool odd = ((uintptr_t)d.base + off) & 1u;
-      uint32_t ip = 0, l4 = 0, st = 0;
-      if (!hdr_ok) {
-        st = MI_ST_MALFORMED;
-      } else {
-        uint32_t sh = fold16(sum_h);
-        if (ih.hl != 20u && odd) sh = swap16(sh);  // in_cksum (stream) vs in_cksum_hdr (abs)
-        ip = ~sh & 0xffffu;
-        if (l4_ok) {
-          uint32_t sl = fold16(sum_l);
-          if (odd) sl = swap16(sl);
-          const uint32_t plen = ih.iplen - ih.hl;
-          const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(plen);
-          l4 = ~fold16_64(seed + sl) & 0xffffu;
-        } else {
-          st = MI_ST_MALFORMED;
-        }
-        st |= (ip ? MI_ST_IP_BAD : 0u) | (l4 ? MI_ST_L4_BAD : 0u);
-      }
-      if (ip_out) ip_out[i] = (uint16_t)ip;
-      if (l4_out) l4_out[i] = (uint16_t)l4;
-      if (st_out) st_out[i] = (uint8_t)st;
-      if (bad && st) atomicAdd(bad, 1u);
-    }
+    if (lane == 0)
+      verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
+                   l4_out, st_out, bad);
   });
+}
+
+// RX verify of a PACKED batch (MI_BATCH_PACKED: offsets ascending, datagrams
+// back to back with gaps < 64 B -- the mixed-length Pareto layout).  A wave
+// owns 64 consecutive datagrams (one per lane for descriptors, header and
+// outputs) and streams their whole byte range as one flat run of 16-byte chunks
+// -- every load a full 1 KiB wave-instruction, no lane idles on a short
+// datagram, no wave waits on a long one.  Each chunk is credited to the
+// datagram(s) it overlaps (binary search over the 64 range ends in LDS, LDS
+// atomic add); datagram totals are < 2^31 (<= 65535 bytes), so L4 = total -
+// header exactly, as in ipv4_sums.  A range whose descriptors are not packed
+// after all falls back to one lane per datagram: always correct, only slower.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
+                                                               uint16_t *l4_out, uint8_t *st_out,
+                                                               uint32_t *bad) {
+  __shared__ uint32_t s_start[kBlock], s_end[kBlock], s_acc[kBlock];
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, sb = wv * 64u;
+  const uint32_t nwaves = gridDim.x * (kBlock / 64);
+  for (uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u; p0 < d.n; p0 += nwaves * 64u) {
+    const uint32_t i = p0 + lane;
+    const bool act = i < d.n;
+    const uint32_t off = act ? pkt_off(d, i) : 0u, flen = act ? pkt_len(d, i) : 0u;
+    // this lane's datagram header window (3 chunks, mostly L2 hits of the run below)
+    u32x4 hv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hv[k] = ld16(r, act && flen ? (off & ~15u) + 16u * k : kOOB);
+    const uint32_t end = act ? off + flen : 0u;
+    const uint32_t prev_end = __shfl_up(end, 1, 64);
+    const bool ok = !act || (off < kOOB && end >= off &&
+                             (lane == 0 || (off >= prev_end && off - prev_end < 64u)));
+    const uint32_t r0 = __builtin_amdgcn_readfirstlane(off) & ~15u;
+    uint32_t r1 = end;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) r1 = max(r1, (uint32_t)__shfl_xor(r1, o, 64));
+    const bool packed = __all(ok);
+    if (!packed || r1 - r0 > (64u << 20)) {
+      // not packed: one lane per datagram, its own loads
+      if (act) {
+        u32x4 v[8];
+        issue_first<1, 8>(r, off, flen, 0, v);
+        IpHdr ih;
+        bool hdr_ok, l4_ok;
+        uint32_t sum_h, sum_l;
+        ipv4_sums<1, 8, false>(r, off, flen, 0, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+        verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
+                     l4_out, st_out, bad);
+      }
+      continue;
+    }
+    // header, validity, summed range [off, off + lend)
+    const uint32_t h = off & 15u;
+    const IpHdr ih = parse_ipv4<1, 3>(hv, h);
+    const bool odd = h & 1u;
+    const bool hdr_ok = act && flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+    const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+    const uint32_t hend = hdr_ok ? ih.hl : 0u;
+    const uint32_t lend = l4_ok ? ih.iplen : hend;
+    uint32_t hdr = 0;
+    if (hend == 20u) {
+      hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+            abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+    } else if (hend > 20u) {  // IP options: up to 60 header bytes, 5 chunks
+      const uint32_t c0 = off & ~15u;
+      for (uint32_t k = 0; k < 5; ++k) {
+        const u32x4 x = k < 3 ? hv[k] : ld16(r, c0 + 16u * k);
+        hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
+      }
+    }
+    s_start[sb + lane] = act ? off - r0 : 0xFFFFFFF0u;
+    s_end[sb + lane] = act ? off - r0 + lend : 0xFFFFFFF0u;
+    s_acc[sb + lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t nch = (r1 - r0 + 15u) >> 4;
+    for (uint32_t cb = 0; cb < nch; cb += 64u * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t c = cb + 64u * u + lane;
+        v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t a = 16u * (cb + 64u * u + lane);  // chunk start, relative to r0
+        if (a >= 16u * nch) continue;
+        // first datagram whose summed range ends after a (ends ascend)
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+          if (s_end[sb + k + step - 1] <= a) k += step;
+        while (k < 64u) {
+          const uint32_t st = s_start[sb + k], en = s_end[sb + k];
+          if (st >= a + 16u) break;
+          const uint32_t part = (st <= a && en >= a + 16u)
+                                    ? sum4(v[u])
+                                    : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
+          if (part) atomicAdd(&s_acc[sb + k], part);
+          if (en > a + 16u) break;
+          ++k;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (act) {
+      const uint32_t total = s_acc[sb + lane];
+      verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
+    }
+    __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
+  }
 }
 
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
@@ -695,6 +818,7 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
   d->fixed_len = b->fixed_len;
   d->len_lo = 0;
   d->len_hi = ~0u;
+  d->flags = b->flags;
   return 0;
 }
 
@@ -731,6 +855,14 @@ constexpr uint32_t kClassEdges[] = {0u, 99u, 739u, 2019u, ~0u};
 
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
+  if ((d.flags & MI_BATCH_PACKED) && d.offs && d.lens && !g_tune.g) {
+    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+    uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
+    if (blocks > (uint64_t)cap) blocks = cap;
+    hipLaunchKernelGGL((k_ipv4_verify_packed<8>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock),
+                       0, s, d, ip, l4, st, bad);
+    return launched();
+  }
   if (!d.lens || g_tune.g || max_len < kClassEdges[1])
     return launch_verify_shape(d, pick_shape(max_len), ip, l4, st, bad, s);
   for (int c = 0; c + 1 < (int)(sizeof kClassEdges / sizeof kClassEdges[0]); ++c) {
@@ -1036,6 +1168,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
     hipStream_t st = c.hstream[k];
     Desc d{};
     d.len_hi = ~0u;
+    d.flags = b->flags;
     d.base = c.dstage[k];
     d.bytes = (uint32_t)((end - s0 + 15u) & ~15ull);
     d.n = j - i;

@@ -189,7 +189,8 @@ def test_full_size_config(name):
     assert np.array_equal(st, st_o)
 
 
-def test_pareto_mixed():
+@pytest.mark.parametrize("packed", [False, True])
+def test_pareto_mixed(packed):
     """Mixed 64-9000 B (Pareto) batch packed at 8-byte offsets."""
     n = 1 << 16
     lens = synth.pareto_lengths(n)
@@ -199,11 +200,19 @@ def test_pareto_mixed():
     _, ref = aligned(host)
     ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32), nthreads=8)
     buf = dev_tensor(host)
-    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)))
+    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)),
+                    packed=packed)
     mi.ipv4_finalize(b)
     assert np.array_equal(cpu(buf), ref)
     r = mi.ipv4_verify(b)
     assert not cpu(r["status"]).any()
+    fin = cpu(buf)
+    fin[offs[::101].astype(np.int64) + 25] ^= 0x80
+    buf.copy_(torch.from_numpy(fin))
+    r = mi.ipv4_verify(b, bad_count=True)
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(fin, n, offs=offs, flen=lens.astype(np.uint32), nthreads=8)
+    assert np.array_equal(cpu(r["ip"]), ip_o) and np.array_equal(cpu(r["l4"]), l4_o)
+    assert np.array_equal(cpu(r["status"]), st_o) and int(r["bad"].item()) == len(offs[::101])
 
 
 def test_host_path_matches_device():
@@ -280,3 +289,49 @@ def test_every_shape_bit_exact(golden, shape):
             assert sp[i] == ORC.chain_skip([(h[o:o + L].tobytes(), o % 64)], L, 0)
     finally:
         mi.set_shape(0, 0, 0)
+
+
+def test_packed_layout_golden(golden):
+    """MI_BATCH_PACKED (flat ranges of 64 datagrams) on the reference's golden
+    RX batch: runts, options, malformed headers, corrupted packets, odd starts."""
+    g = golden
+    n = len(g["vb_offs"])
+    buf = dev_tensor(g["ver_in"])
+    b = mi.PktBatch(buf, n, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                    lens=dev_tensor(g["vb_flen"].astype(np.int32)), packed=True)
+    r = mi.ipv4_verify(b, bad_count=True)
+    assert np.array_equal(cpu(r["ip"]), g["ver_ip"])
+    assert np.array_equal(cpu(r["l4"]), g["ver_l4"])
+    assert np.array_equal(cpu(r["status"]), g["ver_st"])
+    assert int(r["bad"].item()) == int((g["ver_st"] != 0).sum())
+
+
+@pytest.mark.parametrize("layout", ["packed", "shuffled", "gappy"])
+def test_packed_hint_any_layout(layout):
+    """The packed kernel is exact on real packed batches and falls back (still
+    exact) when the hint is wrong: descending offsets, large gaps."""
+    rng = np.random.default_rng(41)
+    n = 5000
+    lens = synth.pareto_lengths(n, seed=8)
+    offs = synth.packed_offsets(lens, first_off=6)
+    if layout == "gappy":
+        offs = offs + np.arange(n, dtype=np.uint64) * 200
+    b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=9, proto=rng.choice([6, 17], n))
+    host = b0["buf"]
+    _, ref = aligned(host)
+    ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32))
+    bad = rng.choice(n, 40, replace=False)
+    ref[offs[bad].astype(np.int64) + rng.integers(0, 40, 40)] ^= 0x11
+    perm = np.arange(n)
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+    o2, l2 = offs[perm], lens[perm]
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(ref, n, offs=o2, flen=l2.astype(np.uint32))
+    buf = dev_tensor(ref)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(o2.astype(np.int64)), lens=dev_tensor(l2.astype(np.int32)),
+                    packed=True)
+    r = mi.ipv4_verify(b, bad_count=True)
+    assert np.array_equal(cpu(r["ip"]), ip_o)
+    assert np.array_equal(cpu(r["l4"]), l4_o)
+    assert np.array_equal(cpu(r["status"]), st_o)
+    assert int(r["bad"].item()) == int((st_o != 0).sum()) >= 40

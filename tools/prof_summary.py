@@ -21,9 +21,11 @@ import statistics
 from collections import defaultdict
 
 
-def short(name: str) -> str:
-    m = re.search(r"(k_[a-z0-9_]+)", name)
-    return m.group(1) if m else name[:40]
+def short(name: str, templ: bool = False) -> str:
+    m = re.search(r"(k_[a-z0-9_]+)(<[^>]*>)?", name)
+    if not m:
+        return name[:40]
+    return m.group(1) + ((m.group(2) or "") if templ else "")
 
 
 def union_len(iv):
@@ -55,11 +57,12 @@ def main():
     ap.add_argument("--pmc-fetch")
     ap.add_argument("--pmc-write")
     ap.add_argument("--skip-first", type=int, default=0, help="ignore the first N dispatches of the kernel")
+    ap.add_argument("--templates", action="store_true", help="keep template arguments in kernel names")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     per = defaultdict(list)
     for r in rows:
-        per[short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        per[short(r["Kernel_Name"], a.templates)].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     res = {}
     for k, iv in per.items():
         d = [e - s for s, e in iv]
