@@ -506,44 +506,34 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // The run is cut into U-chunk pieces (U x 16 B contiguous); lane j takes
-    // piece j of every 64: its U loads are one contiguous 16*U-byte span, so a
-    // lane crosses few datagram boundaries and credits a datagram once per
-    // crossing (register accumulator, LDS atomic add on change) instead of
-    // once per chunk.
     const uint32_t nch = (r1 - r0 + 15u) >> 4;
-    const uint32_t npiece = (nch + U - 1) / U;
-    for (uint32_t pb = 0; pb < npiece; pb += 64u) {
-      const uint32_t c0 = (pb + lane) * U;  // first chunk of this lane's piece
+    for (uint32_t cb = 0; cb < nch; cb += 64u * U) {
       u32x4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = ld16(r, c0 + u < nch ? r0 + 16u * (c0 + u) : kOOB);
-      if (c0 >= nch) continue;
-      // first datagram whose summed range ends after the piece start (ends ascend)
-      const uint32_t a0 = 16u * c0;
-      uint32_t k = 0;
-#pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1)
-        if (s_end[sb + k + step - 1] <= a0) k += step;
-      uint32_t st = k < 64u ? s_start[sb + k] : ~0u, en = k < 64u ? s_end[sb + k] : ~0u;
-      uint32_t acc = 0;
+      for (int u = 0; u < U; ++u) {
+        const uint32_t c = cb + 64u * u + lane;
+        v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const uint32_t a = a0 + 16u * u;
-        if (c0 + u >= nch) break;
-        // credit this chunk to every datagram it overlaps
-        while (k < 64u && st < a + 16u) {
-          acc += (st <= a && en >= a + 16u) ? sum4(v[u])
-                                            : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
-          if (en > a + 16u) break;  // datagram k continues past this chunk
-          if (acc) atomicAdd(&s_acc[sb + k], acc);
-          acc = 0;
+        const uint32_t a = 16u * (cb + 64u * u + lane);  // chunk start, relative to r0
+        if (a >= 16u * nch) continue;
+        // first datagram whose summed range ends after a (ends ascend)
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t step = 32; step >= 1; step >>= 1)
+          if (s_end[sb + k + step - 1] <= a) k += step;
+        while (k < 64u) {
+          const uint32_t st = s_start[sb + k], en = s_end[sb + k];
+          if (st >= a + 16u) break;
+          const uint32_t part = (st <= a && en >= a + 16u)
+                                    ? sum4(v[u])
+                                    : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
+          if (part) atomicAdd(&s_acc[sb + k], part);
+          if (en > a + 16u) break;
           ++k;
-          st = k < 64u ? s_start[sb + k] : ~0u;
-          en = k < 64u ? s_end[sb + k] : ~0u;
         }
       }
-      if (acc && k < 64u) atomicAdd(&s_acc[sb + k], acc);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
