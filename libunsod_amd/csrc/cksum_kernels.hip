@@ -449,15 +449,16 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
   __shared__ uint32_t s_start[kBlock], s_end[kBlock], s_acc[kBlock];
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, sb = wv * 64u;
-  const uint32_t nwaves = gridDim.x * (kBlock / 64);
-  for (uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u; p0 < d.n; p0 += nwaves * 64u) {
+  const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
+  uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u;
+  if (p0 >= d.n) return;
+  // descriptors of this lane's datagram; the next range's are fetched while
+  // this range is folded
+  uint32_t off = p0 + lane < d.n ? pkt_off(d, p0 + lane) : 0u;
+  uint32_t flen = p0 + lane < d.n ? pkt_len(d, p0 + lane) : 0u;
+  for (;;) {
     const uint32_t i = p0 + lane;
     const bool act = i < d.n;
-    const uint32_t off = act ? pkt_off(d, i) : 0u, flen = act ? pkt_len(d, i) : 0u;
-    // this lane's datagram header window (3 chunks, mostly L2 hits of the run below)
-    u32x4 hv[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) hv[k] = ld16(r, act && flen ? (off & ~15u) + 16u * k : kOOB);
     const uint32_t end = act ? off + flen : 0u;
     const uint32_t prev_end = __shfl_up(end, 1, 64);
     const bool ok = !act || (off < kOOB && end >= off &&
@@ -466,83 +467,104 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     uint32_t r1 = end;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) r1 = max(r1, (uint32_t)__shfl_xor(r1, o, 64));
-    const bool packed = __all(ok);
-    if (!packed || r1 - r0 > (64u << 20)) {
+    const bool packed = __all(ok) && r1 - r0 <= (64u << 20);
+    const uint32_t nch = packed ? (r1 - r0 + 15u) >> 4 : 0u;
+    // first pass of the run and this lane's header window, issued together
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = 64u * u + lane;
+      v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+    }
+    u32x4 hv[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hv[k] = ld16(r, packed && act && flen ? (off & ~15u) + 16u * k : kOOB);
+    const uint32_t pn = p0 + rstride;
+    uint32_t offn = 0, flenn = 0;
+    if (pn + lane < d.n) {
+      offn = pkt_off(d, pn + lane);
+      flenn = pkt_len(d, pn + lane);
+    }
+    if (!packed) {
       // not packed: one lane per datagram, its own loads
       if (act) {
-        u32x4 v[8];
-        issue_first<1, 8>(r, off, flen, 0, v);
+        u32x4 w[8];
+        issue_first<1, 8>(r, off, flen, 0, w);
         IpHdr ih;
         bool hdr_ok, l4_ok;
         uint32_t sum_h, sum_l;
-        ipv4_sums<1, 8, false>(r, off, flen, 0, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+        ipv4_sums<1, 8, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l);
         verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
                      l4_out, st_out, bad);
       }
-      continue;
-    }
-    // header, validity, summed range [off, off + lend)
-    const uint32_t h = off & 15u;
-    const IpHdr ih = parse_ipv4<1, 3>(hv, h);
-    const bool odd = h & 1u;
-    const bool hdr_ok = act && flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-    const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-    const uint32_t hend = hdr_ok ? ih.hl : 0u;
-    const uint32_t lend = l4_ok ? ih.iplen : hend;
-    uint32_t hdr = 0;
-    if (hend == 20u) {
-      hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
-            abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
-    } else if (hend > 20u) {  // IP options: up to 60 header bytes, 5 chunks
-      const uint32_t c0 = off & ~15u;
-      for (uint32_t k = 0; k < 5; ++k) {
-        const u32x4 x = k < 3 ? hv[k] : ld16(r, c0 + 16u * k);
-        hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
-      }
-    }
-    s_start[sb + lane] = act ? off - r0 : 0xFFFFFFF0u;
-    s_end[sb + lane] = act ? off - r0 + lend : 0xFFFFFFF0u;
-    s_acc[sb + lane] = 0u;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t nch = (r1 - r0 + 15u) >> 4;
-    for (uint32_t cb = 0; cb < nch; cb += 64u * U) {
-      u32x4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t c = cb + 64u * u + lane;
-        v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t a = 16u * (cb + 64u * u + lane);  // chunk start, relative to r0
-        if (a >= 16u * nch) continue;
-        // first datagram whose summed range ends after a (ends ascend)
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t step = 32; step >= 1; step >>= 1)
-          if (s_end[sb + k + step - 1] <= a) k += step;
-        while (k < 64u) {
-          const uint32_t st = s_start[sb + k], en = s_end[sb + k];
-          if (st >= a + 16u) break;
-          const uint32_t part = (st <= a && en >= a + 16u)
-                                    ? sum4(v[u])
-                                    : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
-          if (part) atomicAdd(&s_acc[sb + k], part);
-          if (en > a + 16u) break;
-          ++k;
+    } else {
+      // header, validity, summed range [off, off + lend)
+      const uint32_t h = off & 15u;
+      const IpHdr ih = parse_ipv4<1, 3>(hv, h);
+      const bool odd = h & 1u;
+      const bool hdr_ok = act && flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+      const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+      const uint32_t hend = hdr_ok ? ih.hl : 0u;
+      const uint32_t lend = l4_ok ? ih.iplen : hend;
+      uint32_t hdr = 0;
+      if (hend == 20u) {
+        hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+              abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+      } else if (hend > 20u) {  // IP options: up to 60 header bytes, 5 chunks
+        const uint32_t c0 = off & ~15u;
+        for (uint32_t k = 0; k < 5; ++k) {
+          const u32x4 x = k < 3 ? hv[k] : ld16(r, c0 + 16u * k);
+          hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
         }
       }
+      s_start[sb + lane] = act ? off - r0 : 0xFFFFFFF0u;
+      s_end[sb + lane] = act ? off - r0 + lend : 0xFFFFFFF0u;
+      s_acc[sb + lane] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (uint32_t cb = 0;;) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t a = 16u * (cb + 64u * u + lane);  // chunk start, relative to r0
+          if (a >= 16u * nch) continue;
+          // first datagram whose summed range ends after a (ends ascend)
+          uint32_t k = 0;
+#pragma unroll
+          for (uint32_t step = 32; step >= 1; step >>= 1)
+            if (s_end[sb + k + step - 1] <= a) k += step;
+          while (k < 64u) {
+            const uint32_t st = s_start[sb + k], en = s_end[sb + k];
+            if (st >= a + 16u) break;
+            const uint32_t part = (st <= a && en >= a + 16u)
+                                      ? sum4(v[u])
+                                      : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
+            if (part) atomicAdd(&s_acc[sb + k], part);
+            if (en > a + 16u) break;
+            ++k;
+          }
+        }
+        cb += 64u * U;
+        if (cb >= nch) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t c = cb + 64u * u + lane;
+          v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (act) {
+        const uint32_t total = s_acc[sb + lane];
+        verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
+      }
+      __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (act) {
-      const uint32_t total = s_acc[sb + lane];
-      verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
-    }
-    __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
+    if (pn >= d.n) break;
+    p0 = pn;
+    off = offn;
+    flen = flenn;
   }
 }
 
