@@ -442,11 +442,32 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 // atomic add); datagram totals are < 2^31 (<= 65535 bytes), so L4 = total -
 // header exactly, as in ipv4_sums.  A range whose descriptors are not packed
 // after all falls back to one lane per datagram: always correct, only slower.
+constexpr uint32_t kOwnCap = 4096;  // ownership-table chunks per wave (64 KiB of run)
+
+// tab[c] = val for c in [c0, c1): byte stores to a 4-byte boundary, dword
+// stores to a 16-byte boundary, 16-byte stores, then the tails.
+__device__ __forceinline__ void fill_run(uint8_t *tab, uint32_t c0, uint32_t c1, uint8_t val) {
+  const uint32_t w = val * 0x01010101u;
+  uint32_t c = c0;
+  for (; c < c1 && (c & 3u); ++c) tab[c] = val;
+  for (; c + 4u <= c1 && (c & 15u); c += 4u) *reinterpret_cast<uint32_t *>(tab + c) = w;
+  for (; c + 16u <= c1; c += 16u) *reinterpret_cast<u32x4 *>(tab + c) = u32x4{w, w, w, w};
+  for (; c + 4u <= c1; c += 4u) *reinterpret_cast<uint32_t *>(tab + c) = w;
+  for (; c < c1; ++c) tab[c] = val;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+
 template <int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
                                                                uint16_t *l4_out, uint8_t *st_out,
                                                                uint32_t *bad) {
   __shared__ uint32_t s_start[kBlock], s_end[kBlock], s_acc[kBlock];
+  __shared__ __attribute__((aligned(16))) uint8_t s_own[kBlock / 64][kOwnCap];
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, sb = wv * 64u;
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
@@ -517,22 +538,62 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
           hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
         }
       }
-      s_start[sb + lane] = act ? off - r0 : 0xFFFFFFF0u;
-      s_end[sb + lane] = act ? off - r0 + lend : 0xFFFFFFF0u;
+      const uint32_t my_start = act ? off - r0 : 0xFFFFFFF0u;
+      const uint32_t my_end = act ? off - r0 + lend : 0xFFFFFFF0u;
+      s_start[sb + lane] = my_start;
+      s_end[sb + lane] = my_end;
       s_acc[sb + lane] = 0u;
+      // Ownership table (runs of up to kOwnCap chunks): own[c] = the first
+      // datagram whose summed range ends after byte 16c, | 0x80 when chunk c
+      // lies wholly inside it.  Lane k writes its own run with 16-byte LDS
+      // stores, so a chunk costs one ds_read_u8 instead of a binary search.
+      uint32_t tab_end = act ? my_end : 0u;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) tab_end = max(tab_end, (uint32_t)__shfl_xor(tab_end, o, 64));
+      tab_end = (tab_end + 15u) >> 4;
+      const bool use_tab = tab_end <= kOwnCap;
+      uint8_t *own = s_own[wv];
+      {
+        const uint32_t pe = __shfl_up(act ? my_end : 0u, 1, 64);
+        const uint32_t prev_end = lane ? pe : 0u;
+        if (use_tab && act) {
+          const uint32_t lo = (prev_end + 15u) >> 4, hi = (my_end + 15u) >> 4;
+          const uint32_t i0 = max(lo, (my_start + 15u) >> 4), i1 = max(i0, min(hi, my_end >> 4));
+          for (uint32_t c = lo; c < i0 && c < hi; ++c) own[c] = (uint8_t)lane;
+          fill_run(own, i0, i1, (uint8_t)(lane | 0x80u));
+          for (uint32_t c = i1; c < hi; ++c) own[c] = (uint8_t)lane;
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       for (uint32_t cb = 0;;) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t a = 16u * (cb + 64u * u + lane);  // chunk start, relative to r0
-          if (a >= 16u * nch) continue;
-          // first datagram whose summed range ends after a (ends ascend)
+          const uint32_t c = cb + 64u * u + lane;
+          const uint32_t a = 16u * c;  // chunk start, relative to r0
           uint32_t k = 0;
+          if (use_tab) {
+            const uint32_t e = c < tab_end ? own[c] : 0x40u;
+            const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
+            if (__all(e == e0) && (e0 & 0x80u)) {
+              // the whole wave-instruction lies inside one datagram
+              const uint32_t t = wave_sum(sum4(v[u]));
+              if (lane == 0) atomicAdd(&s_acc[sb + (e0 & 63u)], t);
+              continue;
+            }
+            if (e & 0x80u) {
+              atomicAdd(&s_acc[sb + (e & 63u)], sum4(v[u]));
+              continue;
+            }
+            k = e;  // a boundary chunk (or 0x40: past every summed range)
+          } else {
+            if (a >= 16u * nch) continue;
+            // first datagram whose summed range ends after a (ends ascend)
 #pragma unroll
-          for (uint32_t step = 32; step >= 1; step >>= 1)
-            if (s_end[sb + k + step - 1] <= a) k += step;
+            for (uint32_t step = 32; step >= 1; step >>= 1)
+              if (s_end[sb + k + step - 1] <= a) k += step;
+          }
           while (k < 64u) {
             const uint32_t st = s_start[sb + k], en = s_end[sb + k];
             if (st >= a + 16u) break;
