@@ -567,6 +567,14 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // Every chunk is credited IN FULL (one sum4, no masks) to each datagram
+      // whose summed range it touches; each datagram then subtracts the bytes of
+      // its head chunk before its start and of its tail chunk after its end,
+      // which it reads itself (its head chunk is hv[0]; the tail chunk is one
+      // more 16-byte load, issued here so it lands during the run).
+      const bool nonempty = act && my_end > my_start;
+      const uint32_t tail_c = nonempty ? (off + lend - 1u) & ~15u : 0u;  // buffer offset
+      const u32x4 tv = ld16(r, nonempty ? tail_c : kOOB);
       for (uint32_t cb = 0;;) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -594,13 +602,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
             for (uint32_t step = 32; step >= 1; step >>= 1)
               if (s_end[sb + k + step - 1] <= a) k += step;
           }
+          const uint32_t full = sum4(v[u]);
           while (k < 64u) {
             const uint32_t st = s_start[sb + k], en = s_end[sb + k];
             if (st >= a + 16u) break;
-            const uint32_t part = (st <= a && en >= a + 16u)
-                                      ? sum4(v[u])
-                                      : range_sum(v[u], (int)a - (int)st, 0, (int)(en - st));
-            if (part) atomicAdd(&s_acc[sb + k], part);
+            if (en > st && full) atomicAdd(&s_acc[sb + k], full);
             if (en > a + 16u) break;
             ++k;
           }
@@ -617,7 +623,14 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (act) {
-        const uint32_t total = s_acc[sb + lane];
+        uint32_t total = 0;
+        if (nonempty) {
+          // head chunk bytes before the datagram, tail chunk bytes after its end
+          const uint32_t head_x = range_sum(hv[0], -(int)h, -(int)h, 0);
+          const int trel = (int)(tail_c - off);  // tail chunk start relative to the datagram
+          const uint32_t tail_x = range_sum(tv, trel, (int)lend, trel + 16);
+          total = s_acc[sb + lane] - head_x - tail_x;
+        }
         verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
       }
       __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
@@ -942,8 +955,17 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
     if (blocks > (uint64_t)cap) blocks = cap;
-    hipLaunchKernelGGL((k_ipv4_verify_packed<8>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock),
-                       0, s, d, ip, l4, st, bad);
+    static const int pu = [] {
+      const char *e = getenv("MI_CKSUM_PACKED_U");
+      return e ? atoi(e) : 8;
+    }();
+    const dim3 grid(blocks ? (unsigned)blocks : 1u);
+    if (pu == 4)
+      hipLaunchKernelGGL((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+    else if (pu == 16)
+      hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+    else
+      hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
     return launched();
   }
   if (!d.lens || g_tune.g || max_len < kClassEdges[1])
