@@ -11,7 +11,7 @@ import ctypes as C
 import os
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libmicksum.so")
+LIB_PATH = os.environ.get("MI_CKSUM_LIB") or os.path.join(LIB_DIR, "libmicksum.so")  # override: A/B builds
 
 MI_SPAN_STREAM = 0
 MI_SPAN_ABS = 1

@@ -433,16 +433,28 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 }
 
 // RX verify of a PACKED batch (MI_BATCH_PACKED: offsets ascending, datagrams
-// back to back with gaps < 64 B -- the mixed-length Pareto layout).  A wave
-// owns 64 consecutive datagrams (one per lane for descriptors, header and
-// outputs) and streams their whole byte range as one flat run of 16-byte chunks
-// -- every load a full 1 KiB wave-instruction, no lane idles on a short
-// datagram, no wave waits on a long one.  Each chunk is credited to the
-// datagram(s) it overlaps (binary search over the 64 range ends in LDS, LDS
-// atomic add); datagram totals are < 2^31 (<= 65535 bytes), so L4 = total -
-// header exactly, as in ipv4_sums.  A range whose descriptors are not packed
-// after all falls back to one lane per datagram: always correct, only slower.
+// back to back with gaps < 64 B -- the mixed-length Pareto layout).
+//
+// A wave owns 64 consecutive datagrams (lane k = datagram k: descriptors,
+// header, outputs) and streams their whole byte run as one flat sequence of
+// 16-byte chunks: every load a full 1 KiB wave-instruction, no lane idles on a
+// short datagram, no wave waits on a long one.  Nothing but the descriptors is
+// needed before the run starts:
+//  * an ownership table in LDS (one byte per chunk, written by the datagrams'
+//    own lanes with 16-byte stores) maps a chunk to the first datagram whose
+//    FRAME ends after it, flags chunks wholly inside that frame, and flags the
+//    first three chunks of each frame (its header window);
+//  * an inside chunk costs one unmasked sum4 + one LDS atomic add (one per
+//    wave-instruction when the whole instruction is inside one datagram); only
+//    boundary chunks are masked;
+//  * header-window chunks are copied to LDS as they stream by, so datagram k's
+//    lane parses its header after the run without touching memory again.
+// Frame totals are exact (< 2^31: a datagram is <= 65535 bytes); bytes past
+// ip_len (Ethernet padding, rare) are subtracted afterwards from memory, and
+// L4 = total - header, as in ipv4_sums.  A range whose descriptors are not
+// packed after all falls back to one lane per datagram: always correct.
 constexpr uint32_t kOwnCap = 4096;  // ownership-table chunks per wave (64 KiB of run)
+constexpr uint32_t kOwnIn = 0x80u, kOwnHdr = 0x40u;
 
 // tab[c] = val for c in [c0, c1): byte stores to a 4-byte boundary, dword
 // stores to a 16-byte boundary, 16-byte stores, then the tails.
@@ -468,9 +480,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
                                                                uint32_t *bad) {
   __shared__ uint32_t s_start[kBlock], s_end[kBlock], s_acc[kBlock];
   __shared__ __attribute__((aligned(16))) uint8_t s_own[kBlock / 64][kOwnCap];
+  __shared__ u32x4 s_hdr[kBlock / 64][3][64];
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, sb = wv * 64u;
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
+  uint8_t *own = s_own[wv];
   uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u;
   if (p0 >= d.n) return;
   // descriptors of this lane's datagram; the next range's are fetched while
@@ -488,18 +502,15 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     uint32_t r1 = end;
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) r1 = max(r1, (uint32_t)__shfl_xor(r1, o, 64));
-    const bool packed = __all(ok) && r1 - r0 <= (64u << 20);
-    const uint32_t nch = packed ? (r1 - r0 + 15u) >> 4 : 0u;
-    // first pass of the run and this lane's header window, issued together
+    const uint32_t nch = (r1 - r0 + 15u) >> 4;
+    const bool packed = __all(ok) && nch <= kOwnCap;
+    // first pass of the run, issued before anything else
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t c = 64u * u + lane;
-      v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+      v[u] = ld16(r, packed && c < nch ? r0 + 16u * c : kOOB);
     }
-    u32x4 hv[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) hv[k] = ld16(r, packed && act && flen ? (off & ~15u) + 16u * k : kOOB);
     const uint32_t pn = p0 + rstride;
     uint32_t offn = 0, flenn = 0;
     if (pn + lane < d.n) {
@@ -507,7 +518,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
       flenn = pkt_len(d, pn + lane);
     }
     if (!packed) {
-      // not packed: one lane per datagram, its own loads
+      // not packed (or a run longer than the table): one lane per datagram
       if (act) {
         u32x4 w[8];
         issue_first<1, 8>(r, off, flen, 0, w);
@@ -519,95 +530,53 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
                      l4_out, st_out, bad);
       }
     } else {
-      // header, validity, summed range [off, off + lend)
-      const uint32_t h = off & 15u;
-      const IpHdr ih = parse_ipv4<1, 3>(hv, h);
-      const bool odd = h & 1u;
-      const bool hdr_ok = act && flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-      const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-      const uint32_t hend = hdr_ok ? ih.hl : 0u;
-      const uint32_t lend = l4_ok ? ih.iplen : hend;
-      uint32_t hdr = 0;
-      if (hend == 20u) {
-        hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
-              abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
-      } else if (hend > 20u) {  // IP options: up to 60 header bytes, 5 chunks
-        const uint32_t c0 = off & ~15u;
-        for (uint32_t k = 0; k < 5; ++k) {
-          const u32x4 x = k < 3 ? hv[k] : ld16(r, c0 + 16u * k);
-          hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
-        }
-      }
-      const uint32_t my_start = act ? off - r0 : 0xFFFFFFF0u;
-      const uint32_t my_end = act ? off - r0 + lend : 0xFFFFFFF0u;
-      s_start[sb + lane] = my_start;
-      s_end[sb + lane] = my_end;
+      // frame ranges [st, en) relative to r0, ascending and disjoint
+      const uint32_t st = act ? off - r0 : 0xFFFFFFF0u;
+      const uint32_t en = act ? end - r0 : 0xFFFFFFF0u;
+      s_start[sb + lane] = st;
+      s_end[sb + lane] = en;
       s_acc[sb + lane] = 0u;
-      // Ownership table (runs of up to kOwnCap chunks): own[c] = the first
-      // datagram whose summed range ends after byte 16c, | 0x80 when chunk c
-      // lies wholly inside it.  Lane k writes its own run with 16-byte LDS
-      // stores, so a chunk costs one ds_read_u8 instead of a binary search.
-      uint32_t tab_end = act ? my_end : 0u;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) tab_end = max(tab_end, (uint32_t)__shfl_xor(tab_end, o, 64));
-      tab_end = (tab_end + 15u) >> 4;
-      const bool use_tab = tab_end <= kOwnCap;
-      uint8_t *own = s_own[wv];
-      {
-        const uint32_t pe = __shfl_up(act ? my_end : 0u, 1, 64);
-        const uint32_t prev_end = lane ? pe : 0u;
-        if (use_tab && act) {
-          const uint32_t lo = (prev_end + 15u) >> 4, hi = (my_end + 15u) >> 4;
-          const uint32_t i0 = max(lo, (my_start + 15u) >> 4), i1 = max(i0, min(hi, my_end >> 4));
-          for (uint32_t c = lo; c < i0 && c < hi; ++c) own[c] = (uint8_t)lane;
-          fill_run(own, i0, i1, (uint8_t)(lane | 0x80u));
-          for (uint32_t c = i1; c < hi; ++c) own[c] = (uint8_t)lane;
-        }
+      if (act) {
+        const uint32_t pe = lane ? prev_end - r0 : 0u;
+        const uint32_t lo = (pe + 15u) >> 4, hi = (en + 15u) >> 4;
+        const uint32_t i0 = max(lo, (st + 15u) >> 4), i1 = max(i0, min(hi, en >> 4));
+        for (uint32_t c = lo; c < i0 && c < hi; ++c) own[c] = (uint8_t)lane;
+        fill_run(own, i0, i1, (uint8_t)(lane | kOwnIn));
+        for (uint32_t c = i1; c < hi; ++c) own[c] = (uint8_t)lane;
+        for (uint32_t c = st >> 4; c < min(hi, (st >> 4) + 3u); ++c) own[c] |= (uint8_t)kOwnHdr;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // Every chunk is credited IN FULL (one sum4, no masks) to each datagram
-      // whose summed range it touches; each datagram then subtracts the bytes of
-      // its head chunk before its start and of its tail chunk after its end,
-      // which it reads itself (its head chunk is hv[0]; the tail chunk is one
-      // more 16-byte load, issued here so it lands during the run).
-      const bool nonempty = act && my_end > my_start;
-      const uint32_t tail_c = nonempty ? (off + lend - 1u) & ~15u : 0u;  // buffer offset
-      const u32x4 tv = ld16(r, nonempty ? tail_c : kOOB);
       for (uint32_t cb = 0;;) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t c = cb + 64u * u + lane;
           const uint32_t a = 16u * c;  // chunk start, relative to r0
-          uint32_t k = 0;
-          if (use_tab) {
-            const uint32_t e = c < tab_end ? own[c] : 0x40u;
-            const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
-            if (__all(e == e0) && (e0 & 0x80u)) {
-              // the whole wave-instruction lies inside one datagram
-              const uint32_t t = wave_sum(sum4(v[u]));
-              if (lane == 0) atomicAdd(&s_acc[sb + (e0 & 63u)], t);
-              continue;
-            }
-            if (e & 0x80u) {
-              atomicAdd(&s_acc[sb + (e & 63u)], sum4(v[u]));
-              continue;
-            }
-            k = e;  // a boundary chunk (or 0x40: past every summed range)
-          } else {
-            if (a >= 16u * nch) continue;
-            // first datagram whose summed range ends after a (ends ascend)
-#pragma unroll
-            for (uint32_t step = 32; step >= 1; step >>= 1)
-              if (s_end[sb + k + step - 1] <= a) k += step;
+          const uint32_t e = c < nch ? own[c] : 0u;
+          const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
+          if (__all(e == e0) && (e0 & (kOwnIn | kOwnHdr)) == kOwnIn && cb + 64u * u + 63u < nch) {
+            // the whole wave-instruction lies inside one datagram
+            const uint32_t t = wave_sum(sum4(v[u]));
+            if (lane == 0) atomicAdd(&s_acc[sb + (e0 & 63u)], t);
+            continue;
           }
-          const uint32_t full = sum4(v[u]);
+          if (c >= nch) continue;
+          uint32_t k = e & 63u;
+          if (e & kOwnIn) {
+            atomicAdd(&s_acc[sb + k], sum4(v[u]));
+            if (e & kOwnHdr) s_hdr[wv][c - (s_start[sb + k] >> 4)][k] = v[u];
+            continue;
+          }
+          // boundary chunk: every datagram it touches gets its masked share
           while (k < 64u) {
-            const uint32_t st = s_start[sb + k], en = s_end[sb + k];
-            if (st >= a + 16u) break;
-            if (en > st && full) atomicAdd(&s_acc[sb + k], full);
-            if (en > a + 16u) break;
+            const uint32_t ks = s_start[sb + k], ke = s_end[sb + k];
+            if (ks >= a + 16u) break;
+            const uint32_t part = range_sum(v[u], (int)a - (int)ks, 0, (int)(ke - ks));
+            if (part) atomicAdd(&s_acc[sb + k], part);
+            const uint32_t j = c - (ks >> 4);
+            if (j < 3u) s_hdr[wv][j][k] = v[u];
+            if (ke > a + 16u) break;
             ++k;
           }
         }
@@ -623,13 +592,28 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (act) {
-        uint32_t total = 0;
-        if (nonempty) {
-          // head chunk bytes before the datagram, tail chunk bytes after its end
-          const uint32_t head_x = range_sum(hv[0], -(int)h, -(int)h, 0);
-          const int trel = (int)(tail_c - off);  // tail chunk start relative to the datagram
-          const uint32_t tail_x = range_sum(tv, trel, (int)lend, trel + 16);
-          total = s_acc[sb + lane] - head_x - tail_x;
+        const uint32_t h = off & 15u;
+        const u32x4 hv[3] = {s_hdr[wv][0][lane], s_hdr[wv][1][lane], s_hdr[wv][2][lane]};
+        const IpHdr ih = parse_ipv4<1, 3>(hv, h);
+        const bool odd = h & 1u;
+        const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+        const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+        const uint32_t hend = hdr_ok ? ih.hl : 0u;
+        const uint32_t lend = l4_ok ? ih.iplen : hend;
+        uint32_t total = s_acc[sb + lane];  // bytes [off, off + flen)
+        uint32_t hdr = 0;
+        if (hend == 20u) {
+          hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+                abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+        } else if (hend > 20u) {  // IP options (rare): up to 60 header bytes, 5 chunks
+          for (uint32_t k = 0; k < 5; ++k) {
+            const u32x4 x = k < 3 ? hv[k] : ld16(r, (off & ~15u) + 16u * k);
+            hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
+          }
+        }
+        if (lend < flen) {  // bytes past ip_len (Ethernet padding, malformed): rare
+          for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
+            total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
         }
         verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
       }
