@@ -87,10 +87,25 @@ __device__ __forceinline__ uint32_t range_sum(const u32x4 &v, int rel, int r0, i
   return s;
 }
 
+// x of lane i + n within its 16-lane row (0 past the row end): DPP row_shl.
+template <int N>
+__device__ __forceinline__ uint32_t row_shl(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + N, 0xf, 0xf, false);
+}
+
+// Sum of the G lanes of this lane's group, valid in the group's LEADER lane
+// (lane % G == 0) only.  DPP row shifts inside a 16-lane row (plain VALU ops,
+// no LDS round trip), one cross-row step for G = 32 / 64.
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
-#pragma unroll
-  for (int o = G / 2; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+  if constexpr (G >= 2) x += row_shl<1>(x);
+  if constexpr (G >= 4) x += row_shl<2>(x);
+  if constexpr (G >= 8) x += row_shl<4>(x);
+  if constexpr (G >= 16) x += row_shl<8>(x);
+  if constexpr (G == 32) x += __shfl_down(x, 16, 64);
+  if constexpr (G == 64)
+    x = __builtin_amdgcn_readlane(x, 0) + __builtin_amdgcn_readlane(x, 16) +
+        __builtin_amdgcn_readlane(x, 32) + __builtin_amdgcn_readlane(x, 48);
   return x;
 }
 
@@ -468,11 +483,8 @@ __device__ __forceinline__ void fill_run(uint8_t *tab, uint32_t c0, uint32_t c1,
   for (; c < c1; ++c) tab[c] = val;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
-}
+// Sum over the wave, uniform (every lane gets it).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return group_sum<64>(x); }
 
 template <int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
@@ -553,6 +565,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
         for (int u = 0; u < U; ++u) {
           const uint32_t c = cb + 64u * u + lane;
           const uint32_t a = 16u * c;  // chunk start, relative to r0
+#ifdef MI_EXP_NOCREDIT
+          if (c < nch) s_acc[sb + lane] += sum4(v[u]);
+          continue;
+#endif
           const uint32_t e = c < nch ? own[c] : 0u;
           const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
           if (__all(e == e0) && (e0 & (kOwnIn | kOwnHdr)) == kOwnIn && cb + 64u * u + 63u < nch) {
@@ -569,6 +585,9 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
             continue;
           }
           // boundary chunk: every datagram it touches gets its masked share
+#ifdef MI_EXP_NOBOUND
+          continue;
+#endif
           while (k < 64u) {
             const uint32_t ks = s_start[sb + k], ke = s_end[sb + k];
             if (ks >= a + 16u) break;
