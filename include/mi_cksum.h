@@ -142,6 +142,40 @@ typedef struct mi_span_seeds {
 int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_seeds *seeds,
                         uint16_t *out, void *stream);
 
+/*
+ * Scatter-gather: checksums over mbuf chains, batched (the TX socket-buffer
+ * chains of 2-4 KiB clusters, jumbo frames over several rte_mbufs).  Every
+ * segment's bytes sit in one device buffer; packet i's chain is segments
+ * [pkt_seg[i], pkt_seg[i+1]) -- pkt_seg has n + 1 entries -- with
+ * seg_off[k] / seg_len[k] standing for m_data / m_len (mbuf.h:166-168).
+ *   MI_CHAIN_SKIP:   out[i] = in_cksum_skip(chain_i, len[i], skip[i])
+ *   MI_CHAIN_PSEUDO: out[i] = in_cksum_pseudo_header(chain_i, len[i] (plen),
+ *                             skip[i] (off0), src[i], dst[i], proto[i])
+ * with the reference's walk: leading skip across segments, zero-length mbufs
+ * ignored, a short chain truncates silently (in_cksum.c:193-276).  All arrays
+ * are device pointers.  max_seg: longest segment (0 = unknown).
+ */
+#define MI_CHAIN_SKIP   0u
+#define MI_CHAIN_PSEUDO 1u
+typedef struct mi_chain_batch {
+	void           *base;
+	uint64_t        bytes;
+	const uint64_t *seg_off;
+	const int32_t  *seg_len;
+	const uint32_t *pkt_seg;
+	uint32_t        n;
+	uint32_t        mode;
+	const int32_t  *len;
+	const int32_t  *skip;
+	const uint32_t *src;
+	const uint32_t *dst;
+	const uint8_t  *proto;
+	uint32_t        max_seg;
+	uint32_t        reserved;
+} mi_chain_batch;
+
+int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);
+
 /* Per-packet status bits (the observable outputs the reference counts:
  * ips_badsum ip_input.c:469, tcps_rcvbadsum tcp_input.c:717-720). */
 #define MI_ST_IP_BAD    1u
@@ -162,6 +196,29 @@ int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_see
  */
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                          uint8_t *status, uint32_t *bad_count, void *stream);
+
+/*
+ * RX offload at the driver's batch point (uinet_if_dpdk.c:854-879, before
+ * uinet_pd_deliver_to_stack): verify the burst and produce, per datagram, the
+ * m_pkthdr.csum_flags / csum_data a checksumming NIC would set, so the stack's
+ * unchanged call sites take the offload branch with identical accept/drop
+ * decisions and counters (ip_input.c:459-460, tcp_input.c:698-709,
+ * udp_usrreq.c:431-438; if_loop.c:255-276 sets the same bits):
+ *   well-formed header (see mi_cksum_ipv4_verify): CSUM_IP_CHECKED, plus
+ *     CSUM_IP_VALID iff the header checksum verifies;
+ *   TCP, or UDP with uh_ulen == ip_len - hl, not a fragment, ip_len <= flen:
+ *     CSUM_DATA_VALID | CSUM_PSEUDO_HDR, csum_data = l4 ^ 0xffff (the folded
+ *     pseudo-header sum; the stack's csum_data ^ 0xffff is then exactly
+ *     in_cksum_pseudo_header's result);
+ *   anything else: no flags, csum_data = 0 (the stack computes as before).
+ * Values are mbuf.h:281-305's.  csum_data may be NULL; bad_count as above.
+ */
+#define MI_CSUM_IP_CHECKED 0x0100u
+#define MI_CSUM_IP_VALID   0x0200u
+#define MI_CSUM_DATA_VALID 0x0400u
+#define MI_CSUM_PSEUDO_HDR 0x0800u
+int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
+                        uint32_t *bad_count, void *stream);
 
 /*
  * Back-to-back submission (the RX burst loop, and the bench): launch `steps`

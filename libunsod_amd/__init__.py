@@ -7,15 +7,15 @@ reference interface in Python for tests and the bench.
 """
 from ._lib import (LIB_PATH, MI_SPAN_ABS, MI_SPAN_STREAM, MI_ST_IP_BAD, MI_ST_L4_BAD, MI_ST_MALFORMED,
                    MiCksumError, load)
-from .api import (MbufChain, PktBatch, device_count, host_register, host_unregister, in_addword, in_cksum,
+from .api import (ChainBatch, MbufChain, chain_batch, PktBatch, device_count, host_register, host_unregister, in_addword, in_cksum,
                   in_cksum_hdr, in_cksum_pseudo_header, in_cksum_skip, in_pseudo, init, ipv4_finalize,
-                  ipv4_verify, ipv4_verify_host, ipv4_verify_repeat, set_shape, span_batch, synth_ipv4, version)
+                  ipv4_verify, ipv4_verify_host, ipv4_verify_repeat, rx_offload, set_shape, span_batch, synth_ipv4, version)
 
 load()
 
 __all__ = [
     "LIB_PATH", "MI_SPAN_ABS", "MI_SPAN_STREAM", "MI_ST_IP_BAD", "MI_ST_L4_BAD", "MI_ST_MALFORMED",
-    "MiCksumError", "load", "MbufChain", "PktBatch", "device_count", "host_register", "host_unregister",
+    "MiCksumError", "load", "ChainBatch", "MbufChain", "chain_batch", "PktBatch", "device_count", "host_register", "host_unregister",
     "in_addword", "in_cksum", "in_cksum_hdr", "in_cksum_pseudo_header", "in_cksum_skip", "in_pseudo", "init",
-    "ipv4_finalize", "ipv4_verify", "ipv4_verify_host", "ipv4_verify_repeat", "span_batch", "synth_ipv4", "version",
+    "ipv4_finalize", "ipv4_verify", "ipv4_verify_host", "ipv4_verify_repeat", "rx_offload", "span_batch", "synth_ipv4", "version",
 ]

@@ -22,6 +22,12 @@ MI_BATCH_PACKED = 1
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2
+MI_CHAIN_SKIP = 0
+MI_CHAIN_PSEUDO = 1
+MI_CSUM_IP_CHECKED = 0x100
+MI_CSUM_IP_VALID = 0x200
+MI_CSUM_DATA_VALID = 0x400
+MI_CSUM_PSEUDO_HDR = 0x800
 
 
 class MiCksumError(RuntimeError):
@@ -53,6 +59,26 @@ class SpanSeedsC(C.Structure):
     _fields_ = [(k, C.c_void_p) for k in ("seeds", "src", "dst", "proto", "plens")]
 
 
+class ChainBatchC(C.Structure):
+    """struct mi_chain_batch (include/mi_cksum.h)."""
+    _fields_ = [
+        ("base", C.c_void_p),
+        ("bytes", C.c_uint64),
+        ("seg_off", C.c_void_p),
+        ("seg_len", C.c_void_p),
+        ("pkt_seg", C.c_void_p),
+        ("n", C.c_uint32),
+        ("mode", C.c_uint32),
+        ("len", C.c_void_p),
+        ("skip", C.c_void_p),
+        ("src", C.c_void_p),
+        ("dst", C.c_void_p),
+        ("proto", C.c_void_p),
+        ("max_seg", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
 # Every symbol include/mi_cksum.h declares -> (restype, argtypes).
 SIGNATURES = {
     "in_cksum_skip": (C.c_ushort, [C.c_void_p, C.c_int, C.c_int]),
@@ -67,9 +93,11 @@ SIGNATURES = {
     "mi_cksum_set_shape": (C.c_int, [C.c_int, C.c_int, C.c_int]),
     "mi_cksum_span_batch": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(SpanSeedsC), C.c_void_p,
                                       C.c_void_p]),
+    "mi_cksum_chain_batch": (C.c_int, [C.POINTER(ChainBatchC), C.c_void_p, C.c_void_p]),
     "mi_cksum_ipv4_verify": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
     "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
+    "mi_cksum_rx_offload": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
                                               C.c_uint32, C.c_uint32, C.POINTER(C.c_float),

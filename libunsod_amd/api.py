@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_PACKED, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
                    SpanSeedsC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -156,6 +156,26 @@ def ipv4_verify(b: PktBatch, *, ip: bool = True, l4: bool = True, status: bool =
     return res
 
 
+def rx_offload(b: PktBatch, *, data: bool = True, bad_count: bool = False, out=None, stream=None) -> dict:
+    """RX offload flags for a received burst (mi_cksum_rx_offload): per datagram
+    the m_pkthdr.csum_flags (uint32 -> "flags") and csum_data ("data") that
+    make ip_input / tcp_input / udp_input take their offload branches with
+    unchanged decisions.  Returns a dict of device int32 tensors (u32 values)."""
+    torch = _torch()
+    dev = b.buf.device
+    res = dict(out or {})
+    res.setdefault("flags", torch.empty(b.n, dtype=torch.int32, device=dev))
+    if data:
+        res.setdefault("data", torch.empty(b.n, dtype=torch.int32, device=dev))
+    if bad_count:
+        res["bad"] = res.get("bad", torch.zeros(1, dtype=torch.int32, device=dev))
+        res["bad"].zero_()
+    check("mi_cksum_rx_offload",
+          load().mi_cksum_rx_offload(C.byref(b.c), _ptr(res["flags"]), _ptr(res.get("data")), _ptr(res.get("bad")),
+                                     C.c_void_p(_stream(stream))))
+    return res
+
+
 def ipv4_finalize(b: PktBatch, stream=None) -> None:
     """TX finalize in place (in_delayed_cksum ip_output.c:958-983 + ip_sum :667-672)."""
     check("mi_cksum_ipv4_finalize", load().mi_cksum_ipv4_finalize(C.byref(b.c), C.c_void_p(_stream(stream))))
@@ -171,6 +191,64 @@ def span_batch(b: PktBatch, lanes: int = MI_SPAN_STREAM, *, seeds=None, src=None
     s = SpanSeedsC(*[_ptr(x) for x in keep])
     check("mi_cksum_span_batch",
           load().mi_cksum_span_batch(C.byref(b.c), lanes, C.byref(s), out.data_ptr(), C.c_void_p(_stream(stream))))
+    return out
+
+
+class ChainBatch:
+    """n mbuf chains gathered into one device buffer (mi_chain_batch).
+
+    ``chains[i]`` is a list of segments, each ``bytes`` or ``(bytes, addr_mod)``
+    as for ``MbufChain``; segment data is laid out back to back in a device
+    uint8 tensor at offsets == addr_mod (mod 64) from the 64-aligned base, so
+    the address parity the reference's swap reacts to is kept.
+    """
+
+    def __init__(self, chains, device="cuda"):
+        torch = _torch()
+        offs, lens, pkt_seg, pos = [], [], [0], 0
+        blobs = []
+        for ch in chains:
+            for seg in ch:
+                data, mod = (seg, 0) if isinstance(seg, (bytes, bytearray, memoryview, np.ndarray)) else seg
+                raw = np.frombuffer(bytes(data), np.uint8)
+                pos += (mod - pos) % 64
+                offs.append(pos)
+                lens.append(raw.size)
+                blobs.append((pos, raw))
+                pos += raw.size
+            pkt_seg.append(len(offs))
+        host = np.zeros(max(pos, 1) + 16, np.uint8)
+        for p, raw in blobs:
+            host[p:p + raw.size] = raw
+        self.n = len(pkt_seg) - 1
+        self.buf = torch.from_numpy(host).to(device)
+        self.seg_off = torch.tensor(offs or [0], dtype=torch.int64, device=device)
+        self.seg_len = torch.tensor(lens or [0], dtype=torch.int32, device=device)
+        self.pkt_seg = torch.tensor(pkt_seg, dtype=torch.int32, device=device)
+        self.max_seg = max(lens) if lens else 0
+
+
+def chain_batch(cb: ChainBatch, length, skip, *, src=None, dst=None, proto=None, out=None, stream=None):
+    """in_cksum_skip(chain_i, length[i], skip[i]) for every chain, or with
+    ``src``/``dst``/``proto`` in_cksum_pseudo_header(chain_i, length[i] (plen),
+    skip[i] (off0), src[i], dst[i], proto[i]) -- in_cksum.c:193-276, batched.
+    Per-packet arguments are device tensors (int32 / uint32 / uint8)."""
+    torch = _torch()
+    dev = cb.buf.device
+    out = torch.empty(cb.n, dtype=torch.uint16, device=dev) if out is None else out
+    pseudo = src is not None
+    keep = [torch.as_tensor(length, device=dev).to(torch.int32).contiguous(),
+            torch.as_tensor(skip, device=dev).to(torch.int32).contiguous()]
+    if pseudo:
+        keep += [torch.as_tensor(src, device=dev).to(torch.int64).to(torch.int32).contiguous(),
+                 torch.as_tensor(dst, device=dev).to(torch.int64).to(torch.int32).contiguous(),
+                 torch.as_tensor(proto, device=dev).to(torch.uint8).contiguous()]
+    c = ChainBatchC(cb.buf.data_ptr(), cb.buf.numel(), cb.seg_off.data_ptr(), cb.seg_len.data_ptr(),
+                    cb.pkt_seg.data_ptr(), cb.n, MI_CHAIN_PSEUDO if pseudo else MI_CHAIN_SKIP,
+                    keep[0].data_ptr(), keep[1].data_ptr(),
+                    *([keep[2].data_ptr(), keep[3].data_ptr(), keep[4].data_ptr()] if pseudo else [None] * 3),
+                    cb.max_seg, 0)
+    check("mi_cksum_chain_batch", load().mi_cksum_chain_batch(C.byref(c), out.data_ptr(), C.c_void_p(_stream(stream))))
     return out
 
 

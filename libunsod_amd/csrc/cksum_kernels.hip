@@ -129,6 +129,7 @@ struct Desc {
   uint32_t fixed_len;
   uint32_t len_lo, len_hi;  // length class filter: only lo <= lens[i] < hi (lens != NULL)
   uint32_t flags;           // MI_BATCH_*
+  uint32_t *cflags, *cdata; // RX offload outputs (m_pkthdr.csum_flags / csum_data), or NULL
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
@@ -401,10 +402,51 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
 
 // RX verify outputs of one datagram from its absolute-lane header / L4 sums
 // (ip_input.c:459-471, tcp_input.c:697-720).
+// RX offload: the m_pkthdr.csum_flags / csum_data a
+// checksumming NIC hands the stack (if_loop.c:255-276 is the in-tree model),
+// chosen so every consumer reaches the decision it would reach computing the
+// sums itself:
+//  * ip_input.c:459-460 takes sum = !(flags & CSUM_IP_VALID): IP_CHECKED for
+//    every well-formed header, IP_VALID iff ip_sum folds to 0;
+//  * tcp_input.c:698-709 / udp_usrreq.c:431-438 take th_sum = csum_data ^ 0xffff
+//    under DATA_VALID|PSEUDO_HDR: csum_data = fold(pseudo + S(l4)) = l4 ^ 0xffff
+//    reproduces in_cksum_pseudo_header's value bit for bit.  Set for TCP, and
+//    for UDP when uh_ulen == ip_len - hl (otherwise udp_input sums uh_ulen
+//    bytes, udp_usrreq.c:406-414); never for fragments (ip_reass sums csum_data of the
+//    pieces, no pseudo header) or other protocols.
+// Malformed headers get no flags: the stack's own length checks drop them.
+__device__ __forceinline__ void rx_offload_store(const Desc &d, __amdgpu_buffer_rsrc_t r, uint32_t i,
+                                                 uint32_t off, const IpHdr &ih, bool hdr_ok,
+                                                 bool l4_ok, uint32_t ip, uint32_t l4) {
+  uint32_t fl = 0, cd = 0;
+  if (hdr_ok) {
+    fl = MI_CSUM_IP_CHECKED | (ip ? 0u : MI_CSUM_IP_VALID);
+    const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
+    const uint32_t plen = ih.iplen - ih.hl;
+    bool l4v = l4_ok && (ip_off & 0x3fffu) == 0u;  // IP_MF | IP_OFFMASK
+    if (l4v && ih.proto == 17u) {
+      const uint32_t u = off + ih.hl + 4u;  // uh_ulen, big-endian
+      const uint32_t ulen = plen >= 8u ? ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, u, 0, 0) << 8) |
+                                             __builtin_amdgcn_raw_buffer_load_b8(r, u + 1u, 0, 0)
+                                       : ~0u;
+      l4v = ulen == plen;
+    } else {
+      l4v = l4v && ih.proto == 6u;
+    }
+    if (l4v) {
+      fl |= MI_CSUM_DATA_VALID | MI_CSUM_PSEUDO_HDR;
+      cd = l4 ^ 0xffffu;
+    }
+  }
+  d.cflags[i] = fl;
+  if (d.cdata) d.cdata[i] = cd;
+}
+
 __device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok,
                                              bool l4_ok, uint32_t sum_h, uint32_t sum_l,
                                              uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
-                                             uint32_t *bad) {
+                                             uint32_t *bad, const Desc &d,
+                                             __amdgpu_buffer_rsrc_t r, uint32_t off) {
   uint32_t ip = 0, l4 = 0, st = 0;
   if (!hdr_ok) {
     st = MI_ST_MALFORMED;
@@ -427,6 +469,7 @@ __device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &
   if (l4_out) l4_out[i] = (uint16_t)l4;
   if (st_out) st_out[i] = (uint8_t)st;
   if (bad && st) atomicAdd(bad, 1u);
+  if (d.cflags) rx_offload_store(d, r, i, off, ih, hdr_ok, l4_ok, ip, l4);
 }
 
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
@@ -443,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
     ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0)
       verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
-                   l4_out, st_out, bad);
+                   l4_out, st_out, bad, d, r, off);
   });
 }
 
@@ -539,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
         uint32_t sum_h, sum_l;
         ipv4_sums<1, 8, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l);
         verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
-                     l4_out, st_out, bad);
+                     l4_out, st_out, bad, d, r, off);
       }
     } else {
       // frame ranges [st, en) relative to r0, ascending and disjoint
@@ -634,7 +677,8 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
           for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
             total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
         }
-        verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad);
+        verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r,
+                     off);
       }
       __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
     }
@@ -729,6 +773,117 @@ __global__ __launch_bounds__(kBlock) void k_synth_hdr(Desc d) {
   const uint32_t seed = fold16_64((uint64_t)src + dst + swap16((len - 20u + 6u) & 0xffffu));
   t[16] = (uint8_t)seed; t[17] = (uint8_t)(seed >> 8);
   t[18] = 0; t[19] = 0;
+}
+
+// ------------------------------------------------------ scatter-gather chains
+//
+// in_cksum_skip / in_cksum_pseudo_header over mbuf chains, batched: packet i's
+// chain is segments [pkt_seg[i], pkt_seg[i+1]) of (seg_off, seg_len) -- m_data
+// and m_len of each mbuf (mbuf.h:166-168).  The group walks the chain exactly
+// like the reference (leading skip, zero-length mbufs ignored, short chain
+// truncates: in_cksum.c:203-229, :254-273), folds each piece with the lane
+// group, and turns its absolute lanes into stream lanes with the reference's
+// (clen ^ addr) & 1 swap (:222-225).
+struct ChainDesc {
+  const uint8_t *base;
+  uint32_t bytes;
+  uint32_t n;
+  const uint64_t *seg_off;
+  const int32_t *seg_len;
+  const uint32_t *pkt_seg;
+  const int32_t *len, *skip;
+  const uint32_t *src, *dst;
+  const uint8_t *proto;
+  uint32_t pseudo;
+};
+
+// Folded absolute-lane sum of bytes [off, off + len); valid in the group leader.
+template <int G, int U>
+__device__ __forceinline__ uint32_t group_fold(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t len,
+                                               int lane) {
+  const uint32_t c0 = off & ~15u, h = off & 15u;
+  const uint32_t nch = len ? (h + len + 15u) >> 4 : 0u;
+  const uint32_t npass = (nch + G * U - 1) / (G * U);
+  uint32_t acc = 0;
+  for (uint32_t p = 0; p < npass; ++p) {
+    u32x4 v[U];
+    issue_pass<G, U>(r, c0, nch, p, lane, v);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
+      const bool pure = rel >= 0 && rel + 16 <= (int)len;
+      acc += pure ? sum4(v[u]) : 0u;
+      if (!pure && rel < (int)len) acc += range_sum(v[u], rel, 0, (int)len);
+    }
+    acc = fold16(acc);
+  }
+  return fold16(group_sum<G>(acc));
+}
+
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
+  Desc d{};
+  d.base = cd.base;
+  d.bytes = cd.bytes;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < cd.n; i += stride) {
+    uint32_t k = cd.pkt_seg[i];
+    const uint32_t kend = cd.pkt_seg[i + 1];
+    uint64_t sum = 0;
+    int64_t clen = 0;
+    // fold one piece of the chain: `mlen` bytes at buffer offset `a`
+    auto piece = [&](uint64_t a, int64_t mlen) {
+      if (mlen <= 0) return;
+      const uint32_t aa = a < kOOB ? (uint32_t)a : kOOB;
+      uint32_t f = group_fold<G, U>(r, aa, (uint32_t)min(mlen, (int64_t)0x7fff0000), lane);
+      if ((clen ^ (int64_t)((uintptr_t)cd.base + aa)) & 1) f = swap16(f);
+      sum += f;
+      clen += mlen;
+    };
+    if (!cd.pseudo) {
+      int64_t skip = cd.skip[i], rem = (int64_t)cd.len[i] - skip;
+      for (; skip && k < kend; ++k) {  // in_cksum.c:204-212
+        const int64_t ml = cd.seg_len[k];
+        if (ml > skip) {
+          const int64_t mlen = min(ml - skip, rem);
+          piece(cd.seg_off[k] + (uint64_t)skip, mlen);
+          rem -= mlen;
+          ++k;
+          skip = 0;
+          break;
+        }
+        skip -= ml;
+      }
+      if (!skip)
+        for (; k < kend && rem > 0; ++k) {  // :214-229
+          const int64_t ml = cd.seg_len[k];
+          if (ml == 0) continue;
+          const int64_t mlen = min(ml, rem);
+          piece(cd.seg_off[k], mlen);
+          rem -= mlen;
+        }
+    } else if (k < kend) {
+      const int64_t plen = cd.len[i], off0 = cd.skip[i];
+      sum = (uint64_t)cd.src[i] + cd.dst[i] + ((uint32_t)cd.proto[i] << 8) +
+            swap16((uint32_t)plen & 0xffffu);  // :252-253
+      int64_t rem = plen, mlen = (int64_t)cd.seg_len[k] - off0;
+      uint64_t a = cd.seg_off[k] + (uint64_t)off0;
+      for (;;) {  // :254-273
+        if (rem < mlen) mlen = rem;
+        piece(a, mlen);
+        rem -= mlen;
+        do {
+          ++k;
+        } while (k < kend && rem && cd.seg_len[k] == 0);
+        if (k >= kend || !rem) break;
+        mlen = cd.seg_len[k];
+        a = cd.seg_off[k];
+      }
+    }
+    if (lane == 0) out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+  }
 }
 
 // Scalar drop-in path: one span in page-locked host memory (read over PCIe).
@@ -918,6 +1073,8 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
   d->len_lo = 0;
   d->len_hi = ~0u;
   d->flags = b->flags;
+  d->cflags = nullptr;
+  d->cdata = nullptr;
   return 0;
 }
 
@@ -1059,6 +1216,44 @@ int mi_cksum_span_batch(const mi_pkt_batch *b, uint32_t lanes, const mi_span_see
   return launch_span(d, pick_shape(batch_max_len(b)), abs_lanes, s, out, (hipStream_t)stream);
 }
 
+int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (!b->n) return 0;
+  if (((uintptr_t)b->base & 15u) != 0) return set_err(-EINVAL, "base %p not 16-byte aligned", b->base);
+  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "chain buffer >= 4 GiB");
+  if (!b->base || !b->seg_off || !b->seg_len || !b->pkt_seg || !b->len || !b->skip || !out)
+    return set_err(-EINVAL, "NULL array");
+  if (b->mode == MI_CHAIN_PSEUDO && (!b->src || !b->dst || !b->proto))
+    return set_err(-EINVAL, "pseudo mode needs src / dst / proto");
+  if (b->mode != MI_CHAIN_SKIP && b->mode != MI_CHAIN_PSEUDO) return set_err(-EINVAL, "mode");
+  ChainDesc cd{};
+  cd.base = (const uint8_t *)b->base;
+  cd.bytes = (uint32_t)((b->bytes + 15u) & ~15ull);
+  cd.n = b->n;
+  cd.seg_off = b->seg_off;
+  cd.seg_len = b->seg_len;
+  cd.pkt_seg = b->pkt_seg;
+  cd.len = b->len;
+  cd.skip = b->skip;
+  cd.src = b->src;
+  cd.dst = b->dst;
+  cd.proto = b->proto;
+  cd.pseudo = b->mode == MI_CHAIN_PSEUDO;
+  const Shape sh = pick_shape(b->max_seg ? b->max_seg : 2048u);
+  const int grid = grid_for(cd.n, sh.g);
+  hipStream_t st = (hipStream_t)stream;
+#define X(G_, U_)                                                                              \
+  if (sh.g == G_ && sh.u == U_) {                                                              \
+    hipLaunchKernelGGL((k_chain<G_, U_>), dim3(grid), dim3(kBlock), 0, st, cd, out);            \
+    return launched();                                                                         \
+  }
+  FOR_GU(X)
+#undef X
+  return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
+}
+
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                          uint8_t *status, uint32_t *bad_count, void *stream) {
   Desc d;
@@ -1068,6 +1263,19 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (!d.n) return 0;
   return launch_verify(d, batch_max_len(b), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
+}
+
+int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
+                        uint32_t *bad_count, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  if (!d.n) return 0;
+  if (!csum_flags) return set_err(-EINVAL, "csum_flags is NULL");
+  d.cflags = csum_flags;
+  d.cdata = csum_data;
+  return launch_verify(d, batch_max_len(b), nullptr, nullptr, nullptr, bad_count, (hipStream_t)stream);
 }
 
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,

@@ -148,3 +148,44 @@ class Oracle:
 
     def skip_repeat(self, buf: np.ndarray, length: int, iters: int) -> int:
         return int(self._repeat(buf.ctypes.data, length, iters))
+
+
+# --- RX offload flags -----------------------------------
+CSUM_IP_CHECKED, CSUM_IP_VALID, CSUM_DATA_VALID, CSUM_PSEUDO_HDR = 0x100, 0x200, 0x400, 0x800  # mbuf.h:290-293
+
+
+def rx_offload_flags(buf: np.ndarray, offs, flen, ip, l4, st):
+    """(csum_flags, csum_data) per datagram from a verify result, restating what
+    makes the stack's offload branches equivalent to its own sums:
+    ip_input.c:459-460 (IP_CHECKED / IP_VALID), tcp_input.c:698-709 and
+    udp_usrreq.c:431-438 (DATA_VALID | PSEUDO_HDR, th_sum = csum_data ^ 0xffff),
+    udp_usrreq.c:406-414 (UDP sums uh_ulen bytes: offload only when it equals
+    ip_len - hl), ip_reass (no offload for fragments)."""
+    n = len(offs)
+    fl = np.zeros(n, np.uint32)
+    cd = np.zeros(n, np.uint32)
+    for i in range(n):
+        if st[i] & 4 and (int(flen[i]) < 20 or not _hdr_ok(buf, int(offs[i]), int(flen[i]))):
+            continue
+        p = int(offs[i])
+        fl[i] = CSUM_IP_CHECKED | (CSUM_IP_VALID if ip[i] == 0 else 0)
+        if st[i] & 4:  # header fine, ip_len out of range
+            continue
+        hl = (int(buf[p]) & 15) * 4
+        iplen = (int(buf[p + 2]) << 8) | int(buf[p + 3])
+        ip_off = (int(buf[p + 6]) << 8) | int(buf[p + 7])
+        proto = int(buf[p + 9])
+        if ip_off & 0x3FFF:
+            continue
+        ok = proto == 6
+        if proto == 17 and iplen - hl >= 8:
+            ok = ((int(buf[p + hl + 4]) << 8) | int(buf[p + hl + 5])) == iplen - hl
+        if ok:
+            fl[i] |= CSUM_DATA_VALID | CSUM_PSEUDO_HDR
+            cd[i] = int(l4[i]) ^ 0xFFFF
+    return fl, cd
+
+
+def _hdr_ok(buf, p, flen):
+    hl = (int(buf[p]) & 15) * 4
+    return hl >= 20 and hl <= flen

@@ -335,3 +335,123 @@ def test_packed_hint_any_layout(layout):
     assert np.array_equal(cpu(r["l4"]), l4_o)
     assert np.array_equal(cpu(r["status"]), st_o)
     assert int(r["bad"].item()) == int((st_o != 0).sum()) >= 40
+
+
+# ------------------------------------------- (f) scatter-gather chain batches
+def _golden_chains(g, pfx):
+    return [chain_segments(g, int(g[pfx + "_seg0"][k]), int(g[pfx + "_nseg"][k])) for k in range(len(g[pfx + "_result"]))]
+
+
+def test_chain_batch_skip_golden(golden):
+    g = golden
+    cb = mi.ChainBatch(_golden_chains(g, "sk"))
+    out = mi.chain_batch(cb, dev_tensor(g["sk_len"].astype(np.int32)), dev_tensor(g["sk_skip"].astype(np.int32)))
+    np.testing.assert_array_equal(cpu(out).astype(np.int64), g["sk_result"].astype(np.int64))
+
+
+def test_chain_batch_pseudo_golden(golden):
+    g = golden
+    cb = mi.ChainBatch(_golden_chains(g, "ps"))
+    out = mi.chain_batch(cb, dev_tensor(g["ps_plen"].astype(np.int32)), dev_tensor(g["ps_off0"].astype(np.int32)),
+                         src=dev_tensor(g["ps_src"].astype(np.int64)), dst=dev_tensor(g["ps_dst"].astype(np.int64)),
+                         proto=dev_tensor(g["ps_proto"].astype(np.uint8)))
+    np.testing.assert_array_equal(cpu(out).astype(np.int64), g["ps_result"].astype(np.int64))
+
+
+def test_chain_batch_walk_edges():
+    """Zero-length mbufs, skips ending exactly on / past a segment boundary,
+    short chains, 64 KiB TSO chains of 2 KiB clusters -- against the port."""
+    rng = np.random.default_rng(0xC4A1)
+    chains, lens, skips = [], [], []
+    for i in range(600):
+        nseg = int(rng.integers(1, 40 if i % 50 == 0 else 6))
+        segs = []
+        for _ in range(nseg):
+            L = 0 if rng.random() < 0.15 else int(rng.choice([1, 2, 3, 15, 16, 17, 2048, int(rng.integers(1, 3000))]))
+            segs.append((rng.integers(0, 256, L, dtype=np.uint8).tobytes(), int(rng.integers(64))))
+        total = sum(len(s) for s, _ in segs)
+        bounds = np.cumsum([len(s) for s, _ in segs])
+        c = rng.random()
+        skip = 0 if c < 0.3 else int(rng.choice(bounds)) if c < 0.6 else int(rng.integers(0, total + 3))
+        length = max(skip, total if rng.random() < 0.5 else int(rng.integers(0, total + 40)))
+        chains.append(segs), lens.append(length), skips.append(skip)
+    for _ in range(8):  # TSO send: 64 KiB in 2 KiB clusters, odd placements
+        segs = [(rng.integers(0, 256, 2048, dtype=np.uint8).tobytes(), int(rng.integers(64))) for _ in range(32)]
+        chains.append(segs), lens.append(65536), skips.append(int(rng.integers(0, 60)))
+    want = np.array([ORC.chain_skip(c, L, s) for c, L, s in zip(chains, lens, skips)], np.int64)
+    cb = mi.ChainBatch(chains)
+    out = mi.chain_batch(cb, dev_tensor(np.array(lens, np.int32)), dev_tensor(np.array(skips, np.int32)))
+    np.testing.assert_array_equal(cpu(out).astype(np.int64), want)
+    # pseudo over the same chains (off0 inside the first mbuf, as tcp_output guarantees)
+    off0 = np.array([min(20, len(c[0][0])) for c in chains], np.int32)
+    plen = np.array([max(0, sum(len(s) for s, _ in c) - o - int(rng.integers(0, 5))) for c, o in zip(chains, off0)],
+                    np.int32)
+    src = rng.integers(0, 2**32, len(chains)); dst = rng.integers(0, 2**32, len(chains))
+    proto = rng.choice([6, 17], len(chains)).astype(np.uint8)
+    want = np.array([ORC.chain_pseudo(c, int(p), int(o), int(s), int(d), int(pr))
+                     for c, p, o, s, d, pr in zip(chains, plen, off0, src, dst, proto)], np.int64)
+    out = mi.chain_batch(cb, dev_tensor(plen), dev_tensor(off0), src=dev_tensor(src.astype(np.int64)),
+                         dst=dev_tensor(dst.astype(np.int64)), proto=dev_tensor(proto))
+    np.testing.assert_array_equal(cpu(out).astype(np.int64), want)
+
+
+# --------------------------------------------- (f) RX offload csum_flags / csum_data
+def _rx_mix(n, seed):
+    """A received burst with everything the flag rules distinguish: TCP, UDP,
+    ICMP and other protocols, IP options, fragments, UDP ulen != ip_len - hl,
+    bad checksums, Ethernet padding, ip_len past the frame, hl < 20."""
+    from oracle.pyoracle import rx_offload_flags  # noqa: F401  (checker)
+    rng = np.random.default_rng(seed)
+    lens = np.where(rng.random(n) < 0.3, rng.integers(28, 200, n), rng.integers(200, 9001, n)).astype(np.int64)
+    proto = rng.choice([6, 6, 6, 17, 17, 1, 47], n)
+    hl = np.where(rng.random(n) < 0.1, rng.choice([24, 40, 60], n), 20)
+    hl = np.minimum(hl, (lens // 4) * 4)
+    offs = synth.packed_offsets(lens + 8, first_off=2)
+    b0 = synth.build_ipv4_batch(n, lens, offs=offs, proto=proto, hl=hl, seed=seed, payload="random")
+    keep, h = aligned(b0["buf"])
+    o = offs.astype(np.int64)
+    frag = rng.random(n) < 0.05
+    for i in np.nonzero(frag)[0]:
+        h[o[i] + 6] = int(rng.choice([0x20, 0x00, 0x21]))  # MF, offset only, both
+        h[o[i] + 7] = int(rng.integers(1, 256)) if h[o[i] + 6] != 0x20 else 0
+    udp_bad = (proto == 17) & (rng.random(n) < 0.2) & (lens - hl >= 8)
+    for i in np.nonzero(udp_bad)[0]:
+        h[o[i] + hl[i] + 5] ^= int(rng.integers(1, 8))
+    ORC.ipv4_finalize_batch(h, n, offs=offs, flen=lens.astype(np.uint32))
+    flen = lens.copy()
+    pad = rng.random(n) < 0.05  # Ethernet padding after ip_len
+    flen[pad] += 8
+    for i in np.nonzero((rng.random(n) < 0.05) & (lens > hl))[0]:  # corrupt a payload byte
+        h[o[i] + int(rng.integers(hl[i], lens[i]))] ^= 0x10
+    for i in np.nonzero(rng.random(n) < 0.03)[0]:  # corrupt the header checksum
+        h[o[i] + 10] ^= 1
+    for i in np.nonzero(rng.random(n) < 0.02)[0]:  # ip_len past the frame
+        h[o[i] + 2] = 0xFF
+    for i in np.nonzero(rng.random(n) < 0.01)[0]:  # hl < 20
+        h[o[i]] = 0x44
+    return keep, h, o, flen.astype(np.uint32)
+
+
+@pytest.mark.parametrize("layout", ["unpacked", "packed"])
+def test_rx_offload_flags(layout):
+    from oracle.pyoracle import CSUM_DATA_VALID, CSUM_IP_CHECKED, CSUM_IP_VALID, rx_offload_flags
+    n = 20000
+    keep, h, o, flen = _rx_mix(n, 0x0FF1 + (layout == "packed"))
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(h, n, offs=o.astype(np.uint64), flen=flen, nthreads=8)
+    want_fl, want_cd = rx_offload_flags(h, o, flen, ip_o, l4_o, st_o)
+    # every rule is exercised
+    assert (want_fl & CSUM_DATA_VALID).any() and ((want_fl & CSUM_IP_CHECKED) & ~want_fl & CSUM_DATA_VALID).any()
+    assert (want_fl == 0).any() and ((want_fl & CSUM_IP_CHECKED) & ~(want_fl & CSUM_IP_VALID)).any()
+    buf = dev_tensor(h)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(o), lens=dev_tensor(flen.astype(np.int32)), packed=layout == "packed")
+    r = mi.rx_offload(b, bad_count=True)
+    fl = cpu(r["flags"]).astype(np.uint32)
+    cd = cpu(r["data"]).astype(np.uint32)
+    np.testing.assert_array_equal(fl, want_fl)
+    np.testing.assert_array_equal(cd, want_cd)
+    assert int(r["bad"].item()) == int((st_o != 0).sum())
+    # the stack's decisions through the offload branch equal its own sums
+    chk = (fl & CSUM_IP_CHECKED) != 0
+    assert np.array_equal(((fl & CSUM_IP_VALID) == 0)[chk], (ip_o != 0)[chk])
+    dv = (fl & CSUM_DATA_VALID) != 0
+    assert np.array_equal((cd ^ 0xFFFF)[dv], l4_o[dv].astype(np.uint32))
