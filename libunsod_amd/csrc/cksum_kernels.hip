@@ -490,56 +490,68 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
   });
 }
 
-// RX verify of a PACKED batch (MI_BATCH_PACKED: offsets ascending, datagrams
-// back to back with gaps < 64 B -- the mixed-length Pareto layout).
+// RX verify of a PACKED batch (MI_BATCH_PACKED: datagrams laid out close
+// together in ascending order -- the mixed-length Pareto layout).
 //
 // A wave owns 64 consecutive datagrams (lane k = datagram k: descriptors,
-// header, outputs) and streams their whole byte run as one flat sequence of
-// 16-byte chunks: every load a full 1 KiB wave-instruction, no lane idles on a
-// short datagram, no wave waits on a long one.  Nothing but the descriptors is
-// needed before the run starts:
-//  * an ownership table in LDS (one byte per chunk, written by the datagrams'
-//    own lanes with 16-byte stores) maps a chunk to the first datagram whose
-//    FRAME ends after it, flags chunks wholly inside that frame, and flags the
-//    first three chunks of each frame (its header window);
-//  * an inside chunk costs one unmasked sum4 + one LDS atomic add (one per
-//    wave-instruction when the whole instruction is inside one datagram); only
-//    boundary chunks are masked;
-//  * header-window chunks are copied to LDS as they stream by, so datagram k's
-//    lane parses its header after the run without touching memory again.
-// Frame totals are exact (< 2^31: a datagram is <= 65535 bytes); bytes past
-// ip_len (Ethernet padding, rare) are subtracted afterwards from memory, and
-// L4 = total - header, as in ipv4_sums.  A range whose descriptors are not
-// packed after all falls back to one lane per datagram: always correct.
-constexpr uint32_t kOwnCap = 4096;  // ownership-table chunks per wave (64 KiB of run)
-constexpr uint32_t kOwnIn = 0x80u, kOwnHdr = 0x40u;
+// header, outputs) and streams their whole byte run [r0, r1) as one flat
+// sequence of 16-byte chunks: every load a full 1 KiB wave-instruction, no
+// lane idles on a short datagram, no wave waits on a long one.
+//
+// Crediting bytes to datagrams is a prefix sum, not a per-chunk lookup: the
+// wave scans its chunk sums (DPP, no LDS atomics), so Q(b) = absolute-lane sum
+// of the run's bytes before b is known at every chunk boundary, and
+//     S(datagram) = Q(end) - Q(start)          (mod 2^32; exact, S < 2^31)
+// Each pass parks its 64*U chunk prefixes in LDS for one lookup by the lanes
+// whose start / end chunk it covers; the partial chunks at both ends come from
+// the lane's own header window and last-chunk loads, issued with the run's
+// first pass.  Any layout works (the run just has to be compact enough to be
+// worth streaming: at most twice the datagram bytes plus 4 KiB); a range that
+// is not falls back to one lane per datagram.  Bytes past ip_len (Ethernet
+// padding) are subtracted afterwards and L4 = total - header, as in ipv4_sums.
 
-// tab[c] = val for c in [c0, c1): byte stores to a 4-byte boundary, dword
-// stores to a 16-byte boundary, 16-byte stores, then the tails.
-__device__ __forceinline__ void fill_run(uint8_t *tab, uint32_t c0, uint32_t c1, uint8_t val) {
-  const uint32_t w = val * 0x01010101u;
-  uint32_t c = c0;
-  for (; c < c1 && (c & 3u); ++c) tab[c] = val;
-  for (; c + 4u <= c1 && (c & 15u); c += 4u) *reinterpret_cast<uint32_t *>(tab + c) = w;
-  for (; c + 16u <= c1; c += 16u) *reinterpret_cast<u32x4 *>(tab + c) = u32x4{w, w, w, w};
-  for (; c + 4u <= c1; c += 4u) *reinterpret_cast<uint32_t *>(tab + c) = w;
-  for (; c < c1; ++c) tab[c] = val;
+// Inclusive prefix sum over the wave: row shifts inside 16-lane rows, then
+// the row_bcast:15 / row_bcast:31 carries across rows.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
 }
 
 // Sum over the wave, uniform (every lane gets it).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return group_sum<64>(x); }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor(x, o, 64));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor(x, o, 64));
+  return __builtin_amdgcn_readfirstlane(x);
+}
+
+// Default-policy 16-byte load: the header / last-chunk loads whose lines the
+// run's nontemporal stream reads again shortly after (served from L2).
+__device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+
 template <int U>
 __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
                                                                uint16_t *l4_out, uint8_t *st_out,
                                                                uint32_t *bad) {
-  __shared__ uint32_t s_start[kBlock], s_end[kBlock], s_acc[kBlock];
-  __shared__ __attribute__((aligned(16))) uint8_t s_own[kBlock / 64][kOwnCap];
-  __shared__ u32x4 s_hdr[kBlock / 64][3][64];
+  constexpr uint32_t W = 64u * U;  // chunks per pass
+  __shared__ uint32_t s_q[kBlock / 64][W];
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6, sb = wv * 64u;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
-  uint8_t *own = s_own[wv];
+  uint32_t *sq = s_q[wv];
   uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u;
   if (p0 >= d.n) return;
   // descriptors of this lane's datagram; the next range's are fetched while
@@ -550,15 +562,12 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     const uint32_t i = p0 + lane;
     const bool act = i < d.n;
     const uint32_t end = act ? off + flen : 0u;
-    const uint32_t prev_end = __shfl_up(end, 1, 64);
-    const bool ok = !act || (off < kOOB && end >= off &&
-                             (lane == 0 || (off >= prev_end && off - prev_end < 64u)));
-    const uint32_t r0 = __builtin_amdgcn_readfirstlane(off) & ~15u;
-    uint32_t r1 = end;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) r1 = max(r1, (uint32_t)__shfl_xor(r1, o, 64));
+    const bool sane = !act || (off < kOOB && end >= off && end <= d.bytes);
+    const uint32_t r0 = wave_min(act ? off : ~0u) & ~15u;
+    const uint32_t r1 = wave_max(end);
     const uint32_t nch = (r1 - r0 + 15u) >> 4;
-    const bool packed = __all(ok) && nch <= kOwnCap;
+    const uint32_t dbytes = wave_sum(act ? min(flen, 0xffffu) : 0u);
+    const bool packed = __all(sane) && (uint64_t)nch * 16u <= 2ull * dbytes + 4096u;
     // first pass of the run, issued before anything else
     u32x4 v[U];
 #pragma unroll
@@ -573,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
       flenn = pkt_len(d, pn + lane);
     }
     if (!packed) {
-      // not packed (or a run longer than the table): one lane per datagram
+      // not packed: one lane per datagram
       if (act) {
         u32x4 w[8];
         issue_first<1, 8>(r, off, flen, 0, w);
@@ -585,84 +594,46 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
                      l4_out, st_out, bad, d, r, off);
       }
     } else {
-      // frame ranges [st, en) relative to r0, ascending and disjoint
-      const uint32_t st = act ? off - r0 : 0xFFFFFFF0u;
-      const uint32_t en = act ? end - r0 : 0xFFFFFFF0u;
-      s_start[sb + lane] = st;
-      s_end[sb + lane] = en;
-      s_acc[sb + lane] = 0u;
-      if (act) {
-        const uint32_t pe = lane ? prev_end - r0 : 0u;
-        const uint32_t lo = (pe + 15u) >> 4, hi = (en + 15u) >> 4;
-        const uint32_t i0 = max(lo, (st + 15u) >> 4), i1 = max(i0, min(hi, en >> 4));
-        for (uint32_t c = lo; c < i0 && c < hi; ++c) own[c] = (uint8_t)lane;
-        fill_run(own, i0, i1, (uint8_t)(lane | kOwnIn));
-        for (uint32_t c = i1; c < hi; ++c) own[c] = (uint8_t)lane;
-        for (uint32_t c = st >> 4; c < min(hi, (st >> 4) + 3u); ++c) own[c] |= (uint8_t)kOwnHdr;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t st = act ? off - r0 : 0u, en = act ? end - r0 : 0u;
+      const uint32_t cs = st >> 4, ce = en >> 4, h = st & 15u, t = en & 15u;
+      // this datagram's header window and last (partial) chunk
+      u32x4 hv[3], tv;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) hv[k] = ld16_keep(r, act ? r0 + 16u * (cs + k) : kOOB);
+      tv = ld16_keep(r, act && t ? r0 + 16u * ce : kOOB);
+      uint32_t carry = 0, qs = 0, qe = 0;
       for (uint32_t cb = 0;;) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t c = cb + 64u * u + lane;
-          const uint32_t a = 16u * c;  // chunk start, relative to r0
-#ifdef MI_EXP_NOCREDIT
-          if (c < nch) s_acc[sb + lane] += sum4(v[u]);
-          continue;
-#endif
-          const uint32_t e = c < nch ? own[c] : 0u;
-          const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
-          if (__all(e == e0) && (e0 & (kOwnIn | kOwnHdr)) == kOwnIn && cb + 64u * u + 63u < nch) {
-            // the whole wave-instruction lies inside one datagram
-            const uint32_t t = wave_sum(sum4(v[u]));
-            if (lane == 0) atomicAdd(&s_acc[sb + (e0 & 63u)], t);
-            continue;
-          }
-          if (c >= nch) continue;
-          uint32_t k = e & 63u;
-          if (e & kOwnIn) {
-            atomicAdd(&s_acc[sb + k], sum4(v[u]));
-            if (e & kOwnHdr) s_hdr[wv][c - (s_start[sb + k] >> 4)][k] = v[u];
-            continue;
-          }
-          // boundary chunk: every datagram it touches gets its masked share
-#ifdef MI_EXP_NOBOUND
-          continue;
-#endif
-          while (k < 64u) {
-            const uint32_t ks = s_start[sb + k], ke = s_end[sb + k];
-            if (ks >= a + 16u) break;
-            const uint32_t part = range_sum(v[u], (int)a - (int)ks, 0, (int)(ke - ks));
-            if (part) atomicAdd(&s_acc[sb + k], part);
-            const uint32_t j = c - (ks >> 4);
-            if (j < 3u) s_hdr[wv][j][k] = v[u];
-            if (ke > a + 16u) break;
-            ++k;
-          }
+          const uint32_t x = sum4(v[u]);  // chunks past the run load as zeros
+          const uint32_t inc = wave_scan(x);
+          sq[64u * u + lane] = carry + inc - x;
+          carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         }
-        cb += 64u * U;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (cs - cb < W) qs = sq[cs - cb];
+        if (ce - cb < W) qe = sq[ce - cb];
+        cb += W;
         if (cb >= nch) break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t c = cb + 64u * u + lane;
           v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
         }
+        __builtin_amdgcn_wave_barrier();  // lookups done before the next pass rewrites s_q
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (ce >= nch) qe = carry;  // end on the run's last chunk boundary
       if (act) {
-        const uint32_t h = off & 15u;
-        const u32x4 hv[3] = {s_hdr[wv][0][lane], s_hdr[wv][1][lane], s_hdr[wv][2][lane]};
         const IpHdr ih = parse_ipv4<1, 3>(hv, h);
         const bool odd = h & 1u;
         const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
         const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
         const uint32_t hend = hdr_ok ? ih.hl : 0u;
         const uint32_t lend = l4_ok ? ih.iplen : hend;
-        uint32_t total = s_acc[sb + lane];  // bytes [off, off + flen)
+        // bytes [off, off + flen) = Q(end) - Q(start)
+        uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(hv[0], 0, 0, (int)h));
         uint32_t hdr = 0;
         if (hend == 20u) {
           hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
@@ -680,7 +651,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
         verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r,
                      off);
       }
-      __builtin_amdgcn_wave_barrier();  // the tables are rewritten by the next range
+      __builtin_amdgcn_wave_barrier();
     }
     if (pn >= d.n) break;
     p0 = pn;
@@ -1117,7 +1088,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     if (blocks > (uint64_t)cap) blocks = cap;
     static const int pu = [] {
       const char *e = getenv("MI_CKSUM_PACKED_U");
-      return e ? atoi(e) : 8;
+      return e ? atoi(e) : 4;
     }();
     const dim3 grid(blocks ? (unsigned)blocks : 1u);
     if (pu == 4)
