@@ -1082,7 +1082,12 @@ constexpr uint32_t kClassEdges[] = {0u, 99u, 739u, 2019u, ~0u};
 
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
-  if ((d.flags & MI_BATCH_PACKED) && d.offs && d.lens && !g_tune.g) {
+  // the flat-run kernel: hinted packed layouts, and fixed slots that hold
+  // little besides the datagram (minimum-size frames: streaming the whole slot
+  // costs no more HBM traffic than reading the datagrams' own lines)
+  const bool dense_slots = !d.offs && !d.lens && d.stride &&
+                           d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
+  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
     if (blocks > (uint64_t)cap) blocks = cap;
