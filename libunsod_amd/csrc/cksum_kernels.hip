@@ -525,15 +525,26 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
 // Sum over the wave, uniform (every lane gets it).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return group_sum<64>(x); }
 
+// Wave-uniform max / min: the scan's DPP ladder with the operation's identity
+// in lanes whose source is out of range, read from lane 63 (no LDS traffic).
+template <typename Op>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t x, uint32_t id, Op op) {
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x111, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x112, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x114, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x118, 0xf, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x142, 0xa, 0xf, false));
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x143, 0xc, 0xf, false));
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
 __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = max(x, (uint32_t)__shfl_xor(x, o, 64));
-  return __builtin_amdgcn_readfirstlane(x);
+  return wave_reduce(x, 0u, [](uint32_t a, uint32_t b) { return max(a, b); });
 }
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = min(x, (uint32_t)__shfl_xor(x, o, 64));
-  return __builtin_amdgcn_readfirstlane(x);
+  return wave_reduce(x, ~0u, [](uint32_t a, uint32_t b) { return min(a, b); });
+}
+__device__ __forceinline__ uint32_t wave_total(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_scan(x), 63);
 }
 
 // Default-policy 16-byte load: the header / last-chunk loads whose lines the
@@ -542,8 +553,13 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
+#ifdef MI_EXP_LB
+#define PACKED_BOUNDS __launch_bounds__(kBlock, MI_EXP_LB)
+#else
+#define PACKED_BOUNDS __launch_bounds__(kBlock)
+#endif
 template <int U>
-__global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
+__global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
                                                                uint16_t *l4_out, uint8_t *st_out,
                                                                uint32_t *bad) {
   constexpr uint32_t W = 64u * U;  // chunks per pass
@@ -566,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     const uint32_t r0 = wave_min(act ? off : ~0u) & ~15u;
     const uint32_t r1 = wave_max(end);
     const uint32_t nch = (r1 - r0 + 15u) >> 4;
-    const uint32_t dbytes = wave_sum(act ? min(flen, 0xffffu) : 0u);
+    const uint32_t dbytes = wave_total(act ? min(flen, 0xffffu) : 0u);
     const bool packed = __all(sane) && (uint64_t)nch * 16u <= 2ull * dbytes + 4096u;
     // first pass of the run, issued before anything else
     u32x4 v[U];
@@ -584,12 +600,12 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_packed(Desc d, uint16_t 
     if (!packed) {
       // not packed: one lane per datagram
       if (act) {
-        u32x4 w[8];
-        issue_first<1, 8>(r, off, flen, 0, w);
+        u32x4 w[4];
+        issue_first<1, 4>(r, off, flen, 0, w);
         IpHdr ih;
         bool hdr_ok, l4_ok;
         uint32_t sum_h, sum_l;
-        ipv4_sums<1, 8, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l);
+        ipv4_sums<1, 4, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l);
         verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
                      l4_out, st_out, bad, d, r, off);
       }
