@@ -168,7 +168,7 @@ def main():
                                                     device=dev if dist and backend == "nccl" else None)
     value = job_bytes / elapsed / GIB
 
-    # Roofline of the dominant kernel (k_ipv4_verify).  Algorithmic bytes per
+    # Roofline of the dominant kernel (k_ipv4_verify*, the one verify_plan names).  Algorithmic bytes per
     # launch = sum(L) read + 5 B written per packet (ip u16, l4 u16, status u8).
     # Average launch duration = GPU span of the timed region (hipEvents on the
     # launch streams) / K: launches on different streams overlap, so this is the
@@ -186,7 +186,7 @@ def main():
             traffic = None
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                kernel="k_ipv4_verify", alg_bytes_per_launch=int(alg_bytes),
+                kernel=mi.verify_plan(batches[0]), alg_bytes_per_launch=int(alg_bytes),
                 avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst)
     # the same kernel alone on one stream, every launch bracketed by events
     # (compare with a single-stream rocprof trace)

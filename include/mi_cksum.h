@@ -197,6 +197,11 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                          uint8_t *status, uint32_t *bad_count, void *stream);
 
+/* Diagnostics: the verify kernel mi_cksum_ipv4_verify launches for this batch
+ * ("k_ipv4_verify_packed<4>", "k_ipv4_verify<16,6>", ...).  Thread-local
+ * string, valid until the next call.  Needs no GPU. */
+const char *mi_cksum_verify_plan(const mi_pkt_batch *b);
+
 /*
  * RX offload at the driver's batch point (uinet_if_dpdk.c:854-879, before
  * uinet_pd_deliver_to_stack): verify the burst and produce, per datagram, the

@@ -156,6 +156,11 @@ def ipv4_verify(b: PktBatch, *, ip: bool = True, l4: bool = True, status: bool =
     return res
 
 
+def verify_plan(b: PktBatch) -> str:
+    """Name of the verify kernel ``ipv4_verify`` launches for ``b`` (diagnostics)."""
+    return load().mi_cksum_verify_plan(C.byref(b.c)).decode()
+
+
 def rx_offload(b: PktBatch, *, data: bool = True, bad_count: bool = False, out=None, stream=None) -> dict:
     """RX offload flags for a received burst (mi_cksum_rx_offload): per datagram
     the m_pkthdr.csum_flags (uint32 -> "flags") and csum_data ("data") that

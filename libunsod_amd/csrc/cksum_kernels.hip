@@ -1096,32 +1096,47 @@ int launch_verify_shape(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uin
 // packet is folded exactly once.
 constexpr uint32_t kClassEdges[] = {0u, 99u, 739u, 2019u, ~0u};
 
-int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
-                  uint32_t *bad, hipStream_t s) {
+// Which verify kernel a batch gets.
+enum PlanKind { kPlanRun, kPlanShape, kPlanClasses };
+struct Plan {
+  PlanKind kind;
+  Shape shape;  // kPlanShape
+  int run_u;    // kPlanRun: chunks per lane per pass
+};
+
+Plan verify_plan(const Desc &d, uint32_t max_len) {
+  static const int pu = [] {
+    const char *e = getenv("MI_CKSUM_PACKED_U");
+    const int u = e ? atoi(e) : 4;
+    return u == 8 || u == 16 ? u : 4;
+  }();
   // the flat-run kernel: hinted packed layouts, and fixed slots that hold
   // little besides the datagram (minimum-size frames: streaming the whole slot
   // costs no more HBM traffic than reading the datagrams' own lines)
   const bool dense_slots = !d.offs && !d.lens && d.stride &&
                            d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
-  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
+  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) return {kPlanRun, {0, 0}, pu};
+  if (!d.lens || g_tune.g || max_len < kClassEdges[1]) return {kPlanShape, pick_shape(max_len), 0};
+  return {kPlanClasses, {0, 0}, 0};
+}
+
+int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
+                  uint32_t *bad, hipStream_t s) {
+  const Plan pl = verify_plan(d, max_len);
+  if (pl.kind == kPlanRun) {
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
     if (blocks > (uint64_t)cap) blocks = cap;
-    static const int pu = [] {
-      const char *e = getenv("MI_CKSUM_PACKED_U");
-      return e ? atoi(e) : 4;
-    }();
     const dim3 grid(blocks ? (unsigned)blocks : 1u);
-    if (pu == 4)
+    if (pl.run_u == 4)
       hipLaunchKernelGGL((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
-    else if (pu == 16)
+    else if (pl.run_u == 16)
       hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
     else
       hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
     return launched();
   }
-  if (!d.lens || g_tune.g || max_len < kClassEdges[1])
-    return launch_verify_shape(d, pick_shape(max_len), ip, l4, st, bad, s);
+  if (pl.kind == kPlanShape) return launch_verify_shape(d, pl.shape, ip, l4, st, bad, s);
   for (int c = 0; c + 1 < (int)(sizeof kClassEdges / sizeof kClassEdges[0]); ++c) {
     if (kClassEdges[c] > max_len) break;
     Desc dc = d;
@@ -1255,6 +1270,20 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (!d.n) return 0;
   return launch_verify(d, batch_max_len(b), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
+}
+
+const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
+  static thread_local char buf[96];
+  Desc d;
+  if (!b || make_desc(b, &d)) return "invalid batch";
+  const Plan pl = verify_plan(d, batch_max_len(b));
+  if (pl.kind == kPlanRun)
+    snprintf(buf, sizeof buf, "k_ipv4_verify_packed<%d>", pl.run_u);
+  else if (pl.kind == kPlanShape)
+    snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);
+  else
+    snprintf(buf, sizeof buf, "k_ipv4_verify x length classes");
+  return buf;
 }
 
 int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,

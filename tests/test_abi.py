@@ -77,3 +77,18 @@ def test_no_cpu_fallback_dropin_aborts():
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
     assert p.returncode != 0
     assert "libmicksum: in_cksum_skip" in p.stderr
+
+
+def test_verify_plan_needs_no_gpu():
+    """The kernel choice is host logic: dense minimum-size slots and hinted
+    packed layouts take the flat-run kernel, roomy slots the lane-group one."""
+    import torch
+    import libunsod_amd as mi
+    buf = torch.zeros(1 << 20, dtype=torch.uint8)
+    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=2176, first_off=142, fixed_len=1500)).startswith("k_ipv4_verify<")
+    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=14, fixed_len=46)) == "k_ipv4_verify_packed<4>"
+    offs = torch.arange(100, dtype=torch.int64) * 300
+    lens = torch.full((100,), 280, dtype=torch.int32)
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<4>"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens)) == "k_ipv4_verify x length classes"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens // 4)) == "k_ipv4_verify<1,8>"
