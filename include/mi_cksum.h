@@ -256,6 +256,61 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
 int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream);
 
 /*
+ * TX checksum offload fused with the driver's copy.
+ * The interface advertises if_hwassist = CSUM_IP | CSUM_TCP | CSUM_UDP, so
+ * ip_output leaves ip_sum = 0 and the L4 field holding the in_pseudo seed
+ * (ip_output.c:649-672, tcp_output.c:1084), and the driver's copy of every
+ * outgoing frame into its rte_mbuf (m_copydata(m, 0, len, rm_data),
+ * uinet_if_dpdk.c:594-597) computes and stores the sums on the way.  The
+ * bytes that reach each slot are exactly what the software stack would put on
+ * the wire:
+ *   pkt_len[i] > room             -> MI_TX_NOBUFS, slot untouched (uinet_if_dpdk.c:585-591)
+ *   chain holds < pkt_len bytes    -> MI_TX_SHORT, slot untouched (m_copydata's KASSERT)
+ *   slot[0, len) = the chain's first len bytes
+ *   IPv4 header at l3_off malformed (hl < 20, hl or ip_len beyond the frame,
+ *   ip_len < hl)                  -> MI_TX_NOSUM, copy only
+ *   csum_flags & (CSUM_TCP|CSUM_UDP): in_delayed_cksum (ip_output.c:958-983):
+ *       c = in_cksum_skip(ip, ip_len, hl), CSUM_UDP: 0 -> 0xffff, stored at
+ *       hl + csum_data iff those 2 bytes lie inside the IP mbuf's m_len (the
+ *       segment holding frame byte l3_off, from there on), else MI_TX_L4_SKIPPED
+ *   csum_flags & CSUM_IP: ip_sum = in_cksum(ip, hl) with ip_sum taken as 0
+ *   (ip_output.c:667-672).  Stores beyond len never reach the slot.
+ * csum_flags NULL: CSUM_IP, plus CSUM_TCP / CSUM_UDP by ip_p; csum_data NULL:
+ * 16 for CSUM_TCP, 6 otherwise (tcp_output.c:1066, udp_usrreq.c:1240).
+ * Segments (m_data = src + seg_off[k], m_len = seg_len[k], negative = 0) must
+ * lie inside [src, src + src_bytes); frame i has segments
+ * [pkt_seg[i], pkt_seg[i+1]) and lands at dst + dst_first + i * dst_stride.
+ * src, dst 16-byte aligned, both < 4 GiB; l3_off <= 64.  status: n bytes.
+ */
+#define MI_CSUM_IP  0x1u
+#define MI_CSUM_TCP 0x2u
+#define MI_CSUM_UDP 0x4u
+#define MI_TX_NOBUFS     1u
+#define MI_TX_SHORT      2u
+#define MI_TX_NOSUM      4u
+#define MI_TX_L4_SKIPPED 8u
+typedef struct mi_tx_batch {
+	const void     *src;
+	uint64_t        src_bytes;
+	const uint64_t *seg_off;
+	const int32_t  *seg_len;
+	const uint32_t *pkt_seg;
+	const uint32_t *pkt_len;
+	const uint32_t *csum_flags;
+	const uint32_t *csum_data;
+	void           *dst;
+	uint64_t        dst_bytes;
+	uint64_t        dst_stride;
+	uint64_t        dst_first;
+	uint32_t        room;
+	uint32_t        l3_off;
+	uint32_t        n;
+	uint32_t        max_len;
+} mi_tx_batch;
+
+int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream);
+
+/*
  * Host-resident batch (the path's real start and end: DPDK mbufs in host
  * memory).  b->base / offs / lens are HOST pointers (page-locked memory gives
  * full PCIe rate).  The batch is cut into chunks that are copied to device

@@ -28,6 +28,13 @@ MI_CSUM_IP_CHECKED = 0x100
 MI_CSUM_IP_VALID = 0x200
 MI_CSUM_DATA_VALID = 0x400
 MI_CSUM_PSEUDO_HDR = 0x800
+MI_CSUM_IP = 0x1
+MI_CSUM_TCP = 0x2
+MI_CSUM_UDP = 0x4
+MI_TX_NOBUFS = 1
+MI_TX_SHORT = 2
+MI_TX_NOSUM = 4
+MI_TX_L4_SKIPPED = 8
 
 
 class MiCksumError(RuntimeError):
@@ -79,6 +86,28 @@ class ChainBatchC(C.Structure):
     ]
 
 
+class TxBatchC(C.Structure):
+    """struct mi_tx_batch (include/mi_cksum.h)."""
+    _fields_ = [
+        ("src", C.c_void_p),
+        ("src_bytes", C.c_uint64),
+        ("seg_off", C.c_void_p),
+        ("seg_len", C.c_void_p),
+        ("pkt_seg", C.c_void_p),
+        ("pkt_len", C.c_void_p),
+        ("csum_flags", C.c_void_p),
+        ("csum_data", C.c_void_p),
+        ("dst", C.c_void_p),
+        ("dst_bytes", C.c_uint64),
+        ("dst_stride", C.c_uint64),
+        ("dst_first", C.c_uint64),
+        ("room", C.c_uint32),
+        ("l3_off", C.c_uint32),
+        ("n", C.c_uint32),
+        ("max_len", C.c_uint32),
+    ]
+
+
 # Every symbol include/mi_cksum.h declares -> (restype, argtypes).
 SIGNATURES = {
     "in_cksum_skip": (C.c_ushort, [C.c_void_p, C.c_int, C.c_int]),
@@ -97,6 +126,7 @@ SIGNATURES = {
     "mi_cksum_ipv4_verify": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                        C.c_void_p]),
     "mi_cksum_ipv4_finalize": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p]),
+    "mi_cksum_tx_copy": (C.c_int, [C.POINTER(TxBatchC), C.c_void_p, C.c_void_p]),
     "mi_cksum_verify_plan": (C.c_char_p, [C.POINTER(PktBatchC)]),
     "mi_cksum_rx_offload": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),

@@ -18,7 +18,7 @@ from typing import Iterable
 import numpy as np
 
 from ._lib import (MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
-                   SpanSeedsC, check, load)
+                   SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
 
@@ -257,6 +257,57 @@ def chain_batch(cb: ChainBatch, length, skip, *, src=None, dst=None, proto=None,
     return out
 
 
+def _to_dev(a, dtype: str, dev):
+    """numpy / list / tensor -> contiguous device tensor of ``dtype`` (u32
+    values wrap into int32, as the C side reads them back as uint32_t)."""
+    if a is None:
+        return None
+    torch = _torch()
+    t = a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(np.asarray(a).astype(np.int64)))
+    return t.to(dev).to(getattr(torch, dtype)).contiguous()
+
+
+class TxBatch:
+    """n outgoing frames, each an mbuf chain inside the device uint8 tensor
+    ``src`` (segments ``seg_off`` / ``seg_len`` = m_data / m_len, frame i =
+    segments [pkt_seg[i], pkt_seg[i+1]), ``pkt_len[i]`` = m_pkthdr.len bytes),
+    to be copied into the rte_mbuf data rooms of ``dst`` at
+    ``dst_first + i*dst_stride`` (``room`` = buf_len) -- mi_tx_batch.
+    ``csum_flags`` / ``csum_data``: m_pkthdr fields (None: by ip_p)."""
+
+    def __init__(self, src, seg_off, seg_len, pkt_seg, pkt_len, dst, *, dst_stride: int, dst_first: int = 0,
+                 room: int | None = None, l3_off: int = 14, csum_flags=None, csum_data=None, max_len: int = 0):
+        dev = src.device
+        self.src, self.dst = src, dst
+        self.seg_off = _to_dev(seg_off, "int64", dev)
+        self.seg_len = _to_dev(seg_len, "int32", dev)
+        self.pkt_seg = _to_dev(pkt_seg, "int32", dev)
+        self.pkt_len = _to_dev(pkt_len, "int32", dev)
+        self.csum_flags = _to_dev(csum_flags, "int32", dev)
+        self.csum_data = _to_dev(csum_data, "int32", dev)
+        self.n = int(self.pkt_len.numel())
+        room = int(dst_stride) if room is None else int(room)
+        self._c = TxBatchC(src.data_ptr(), src.numel(), self.seg_off.data_ptr(), self.seg_len.data_ptr(),
+                           self.pkt_seg.data_ptr(), self.pkt_len.data_ptr(), _ptr(self.csum_flags),
+                           _ptr(self.csum_data), dst.data_ptr(), dst.numel(), int(dst_stride), int(dst_first),
+                           room, int(l3_off), self.n, int(max_len))
+
+    @property
+    def c(self) -> TxBatchC:
+        return self._c
+
+
+def tx_copy(tb: TxBatch, *, status=None, stream=None):
+    """TX checksum offload fused with the driver's copy (mi_cksum_tx_copy):
+    every frame's chain is copied into its slot with ip_sum / the L4 sum
+    filled in as in_delayed_cksum + ip_output would.  Returns the per-frame
+    status (device uint8: MI_TX_* bits)."""
+    torch = _torch()
+    status = torch.empty(tb.n, dtype=torch.uint8, device=tb.src.device) if status is None else status
+    check("mi_cksum_tx_copy", load().mi_cksum_tx_copy(C.byref(tb.c), status.data_ptr(), C.c_void_p(_stream(stream))))
+    return status
+
+
 def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str = "region"):
     """Launch ``steps`` verify passes back to back from native code: pass k over
     batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on the library's
@@ -334,5 +385,5 @@ __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
     "ipv4_verify_host", "ipv4_verify_repeat", "host_register", "host_unregister", "set_shape", "init", "device_count", "version",
-    "MI_SPAN_STREAM", "MI_SPAN_ABS",
+    "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

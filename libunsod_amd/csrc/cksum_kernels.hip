@@ -262,6 +262,26 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
   }
 }
 
+// One pass's chunks of an IPv4 datagram whose first byte sits h bytes into
+// the group's first chunk: acc_t += bytes [0, lend), and for datagrams with IP
+// options acc_h += header bytes [0, hend) (TX: acc_f += the ip_sum field).
+template <int G, int U, bool TX>
+__device__ __forceinline__ void fold_pass(const u32x4 (&v)[U], uint32_t p, int lane, uint32_t h,
+                                          int lend, int hend, bool opts, uint32_t &acc_t,
+                                          uint32_t &acc_h, uint32_t &acc_f) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
+    const bool pure = rel >= 0 && rel + 16 <= lend;
+    acc_t += pure ? sum4(v[u]) : 0u;
+    if (!pure && rel < lend) acc_t += range_sum(v[u], rel, 0, lend);
+    if (opts && rel < hend) {
+      acc_h += range_sum(v[u], rel, 0, hend);
+      if (TX) acc_f += range_sum(v[u], rel, 10, 12);
+    }
+  }
+}
+
 // Sums of one IPv4 datagram: header [0, hl) and L4 [hl, ip_len) (absolute
 // lanes, unfolded group totals), plus the parsed header.  TX excludes the
 // ip_sum field (bytes 10..11) from the header sum.
@@ -289,17 +309,7 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   const bool opts = hend > 20;  // group-uniform
   uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
   for (uint32_t p = 0;;) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int rel = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
-      const bool pure = rel >= 0 && rel + 16 <= lend;
-      acc_t += pure ? sum4(v[u]) : 0u;
-      if (!pure && rel < lend) acc_t += range_sum(v[u], rel, 0, lend);
-      if (opts && rel < hend) {
-        acc_h += range_sum(v[u], rel, 0, hend);
-        if (TX) acc_f += range_sum(v[u], rel, 10, 12);
-      }
-    }
+    fold_pass<G, U, TX>(v, p, lane, h, lend, hend, opts, acc_t, acc_h, acc_f);
     if (++p >= npass) break;
     issue_pass<G, U>(r, c0, nch, p, lane, v);
   }
@@ -873,6 +883,457 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
   }
 }
 
+// ------------------------------------------- TX: fused copy + checksum offload
+//
+// SURVEY.md 8(f) rank 2.  With if_hwassist = CSUM_IP | CSUM_TCP | CSUM_UDP the
+// stack leaves the sums to the device (ip_output.c:649-672) and the driver
+// copies every outgoing frame out of its mbuf chain into an rte_mbuf
+// (m_copydata(m, 0, len, rm_data), uinet_if_dpdk.c:594-597).  Here both are
+// one pass: a lane group per frame gathers the chain into 16-byte chunks
+// aligned to the DESTINATION slot (so stores are whole dwordx4 except at the
+// frame's two ends), folds the IP header and the L4 range from those same
+// registers, patches ip_sum and the L4 sum field (in_delayed_cksum,
+// ip_output.c:958-983: UDP 0 -> 0xffff, stored only if it lies inside the IP
+// mbuf's m_len) into the chunk registers, and stores.  Read L, write L.
+//
+// Gather: lane j of the group builds destination chunk ci = p*G*U + u*G + j.
+// The segment table (m_data, m_len of each mbuf of the chain) sits one
+// segment per lane; a group scan turns lengths into frame positions.  For each
+// chunk the lane keeps the segment holding its first byte ("prim") and, when
+// the chunk straddles a segment boundary, the next non-empty one ("sec"); a
+// chunk touching three or more segments (tiny mbufs) takes a slow loop.  A
+// piece of a segment is read as the two aligned source chunks around it and
+// funnel-shifted (v_alignbyte) into destination alignment; bytes outside the
+// piece are masked off.
+#ifndef TX_WAVES
+#define TX_WAVES 1
+#endif
+struct TxDesc {
+  const uint8_t *src;
+  uint32_t src_bytes;
+  uint32_t n;
+  const uint64_t *seg_off;
+  const int32_t *seg_len;
+  const uint32_t *pkt_seg;
+  const uint32_t *pkt_len;
+  const uint32_t *cflags, *cdata;
+  uint8_t *dst;
+  uint32_t dst_bytes;
+  uint32_t room, l3;
+  uint64_t dst_stride, dst_first;
+  uint8_t *status;
+};
+
+// A DPP move computed by EVERY lane at this point.  A DPP result consumed only
+// under a condition may otherwise be sunk into a branch, where the lanes it
+// reads from are switched off and read back as 0.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_all(uint32_t x) {
+  uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+  asm volatile("" : "+v"(y));
+  return y;
+}
+
+// Inclusive prefix sum inside each G-lane group (DPP, no LDS).
+template <int G>
+__device__ __forceinline__ uint32_t group_scan(uint32_t x) {
+  const uint32_t lg = threadIdx.x & (G - 1);
+  if constexpr (G >= 2) { const uint32_t y = dpp_all<0x111>(x); x += lg >= 1 ? y : 0u; }  // row_shr:1
+  if constexpr (G >= 4) { const uint32_t y = dpp_all<0x112>(x); x += lg >= 2 ? y : 0u; }  // row_shr:2
+  if constexpr (G >= 8) { const uint32_t y = dpp_all<0x114>(x); x += lg >= 4 ? y : 0u; }  // row_shr:4
+  if constexpr (G >= 16) { const uint32_t y = dpp_all<0x118>(x); x += (lg & 15u) >= 8 ? y : 0u; }  // row_shr:8
+  if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  if constexpr (G == 64) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// The 16 bytes at source address a (any alignment): the aligned chunk at
+// a & ~15 and (unless aligned) the next one, funnel-shifted.
+struct Raw2 {
+  u32x4 x, y;
+};
+__device__ __forceinline__ Raw2 ld_pair(__amdgpu_buffer_rsrc_t r, uint32_t a) {
+  const uint32_t A = a & ~15u;
+  return {ld16(r, A), ld16(r, (a & 15u) ? A + 16u : kOOB)};
+}
+__device__ __forceinline__ u32x4 shift2(const u32x4 &x, const u32x4 &y, uint32_t a) {
+  const uint32_t s = a & 15u, b = s & 3u;
+  const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+  uint32_t t[6], z[5];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) t[k] = (s & 8u) ? w[k + 2] : w[k];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) z[k] = (s & 4u) ? t[k + 1] : t[k];
+  return {__builtin_amdgcn_alignbyte(z[1], z[0], b), __builtin_amdgcn_alignbyte(z[2], z[1], b),
+          __builtin_amdgcn_alignbyte(z[3], z[2], b), __builtin_amdgcn_alignbyte(z[4], z[3], b)};
+}
+__device__ __forceinline__ u32x4 shift_pair(const Raw2 &p, uint32_t a) { return shift2(p.x, p.y, a); }
+// Bytes [a, b) of a dword as a mask, 0 <= a, b <= 4 (32-bit shifts only).
+__device__ __forceinline__ uint32_t byte_mask(int a, int b) {
+  const uint32_t lo = a >= 4 ? 0u : 0xffffffffu << (8 * a);
+  const uint32_t hi = b >= 4 ? 0xffffffffu : ~(0xffffffffu << (8 * b));
+  return lo & hi;
+}
+// acc |= bytes [lo, hi) of chunk v (any lo, hi; clamped to the chunk)
+__device__ __forceinline__ void merge_bytes(u32x4 &acc, const u32x4 &v, int lo, int hi) {
+  if (lo <= 0 && hi >= 16) {
+    acc.x |= v.x; acc.y |= v.y; acc.z |= v.z; acc.w |= v.w;
+    return;
+  }
+  acc.x |= v.x & byte_mask(min(max(lo, 0), 4), min(max(hi, 0), 4));
+  acc.y |= v.y & byte_mask(min(max(lo - 4, 0), 4), min(max(hi - 4, 0), 4));
+  acc.z |= v.z & byte_mask(min(max(lo - 8, 0), 4), min(max(hi - 8, 0), 4));
+  acc.w |= v.w & byte_mask(min(max(lo - 12, 0), 4), min(max(hi - 12, 0), 4));
+}
+// Byte b (0..15) of chunk v := x, if 0 <= b < 16.
+__device__ __forceinline__ void put_byte(u32x4 &v, int b, uint32_t x) {
+  if (b < 0 || b >= 16) return;
+  const uint32_t sh = 8u * (b & 3), m = ~(0xffu << sh), y = (x & 0xffu) << sh;
+  const int j = b >> 2;
+  v.x = j == 0 ? (v.x & m) | y : v.x;
+  v.y = j == 1 ? (v.y & m) | y : v.y;
+  v.z = j == 2 ? (v.z & m) | y : v.z;
+  v.w = j == 3 ? (v.w & m) | y : v.w;
+}
+// Store bytes [lo, hi) of chunk v at destination address a (16-aligned).
+__device__ __forceinline__ void store_chunk(__amdgpu_buffer_rsrc_t r, uint32_t a, const u32x4 &v, int lo,
+                                            int hi) {
+  if (lo <= 0 && hi >= 16) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, a, 0, 0);
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int b0 = min(max(lo - 4 * j, 0), 4), b1 = min(max(hi - 4 * j, 0), 4);
+    if (b0 == 0 && b1 == 4) {
+      __builtin_amdgcn_raw_buffer_store_b32(w[j], r, a + 4u * j, 0, 0);
+    } else {
+      for (int m = b0; m < b1; ++m)
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j] >> (8 * m)), r, a + 4u * j + m, 0, 0);
+    }
+  }
+}
+
+// TX sums from the group's absolute-lane accumulators (in_delayed_cksum's
+// in_cksum_skip(m, ip_len, hl) and in_cksum(m, hl) with ip_sum = 0), both
+// returned in every lane of the group.
+template <int G>
+__device__ __forceinline__ void tx_sums(uint32_t acc_t, uint32_t acc_h, uint32_t acc_f, int hend,
+                                        const IpHdr &ih, bool odd, bool udp, uint32_t &c_ip,
+                                        uint32_t &c_l4) {
+  const uint32_t total = group_sum<G>(acc_t);
+  uint32_t hdr, field;
+  if (hend > 20) {
+    hdr = group_sum<G>(acc_h);
+    field = group_sum<G>(acc_f);
+  } else if (hend) {
+    hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+          abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+    field = abs_halves(ih.w[2] & 0xffff0000u, odd);
+  } else {
+    hdr = field = 0u;
+  }
+  uint32_t sh = fold16(hdr - field), sl = fold16(total - hdr);
+  if (odd) {
+    sh = swap16(sh);
+    sl = swap16(sl);
+  }
+  c_ip = ~sh & 0xffffu;
+  c_l4 = ~sl & 0xffffu;
+  if (udp && c_l4 == 0u) c_l4 = 0xffffu;
+  c_ip = group_lane<G>(c_ip, 0);
+  c_l4 = group_lane<G>(c_l4, 0);
+}
+
+// Fold one chunk of an IPv4 datagram whose first byte is rel bytes after the
+// datagram start (fold_pass for a single chunk; bytes outside the piece the
+// chunk carries are zero, so whole-chunk arithmetic stays exact).
+__device__ __forceinline__ void fold_chunk(const u32x4 &v, int rel, int lend, int hend, bool opts,
+                                           uint32_t &acc_t, uint32_t &acc_h, uint32_t &acc_f) {
+  const bool pure = rel >= 0 && rel + 16 <= lend;
+  acc_t += pure ? sum4(v) : 0u;
+  if (!pure && rel < lend) acc_t += range_sum(v, rel, 0, lend);
+  if (opts && rel < hend) {
+    acc_h += range_sum(v, rel, 0, hend);
+    acc_f += range_sum(v, rel, 10, 12);
+  }
+}
+
+// x as held by the next lane of this lane's G-lane group (G = 8 or 16), or,
+// for the group's last lane, by the group's first lane of xn: DPP row shifts.
+template <int G>
+__device__ __forceinline__ uint32_t next_lane(uint32_t x, uint32_t xn, bool last) {
+  static_assert(G == 8 || G == 16, "row-local groups only");
+  const uint32_t in = dpp_all<0x101>(x);             // row_shl:1
+  const uint32_t ed = dpp_all<0x110 + (G - 1)>(xn);  // row_shr:G-1
+  return last ? ed : in;
+}
+template <int G>
+__device__ __forceinline__ u32x4 next_lane4(const u32x4 &x, const u32x4 &xn, bool last) {
+  return {next_lane<G>(x.x, xn.x, last), next_lane<G>(x.y, xn.y, last), next_lane<G>(x.z, xn.z, last),
+          next_lane<G>(x.w, xn.w, last)};
+}
+
+// A piece of one segment: destination chunks [cfirst, clast) carrying frame
+// bytes [pa, pe), the byte at frame position q read from source address q + del.
+struct Piece {
+  uint32_t cfirst, clast, del;
+  int pa, pe;
+};
+
+// Pass p of a piece: each lane loads ONE aligned source chunk per destination
+// chunk ci = cfirst + p*G*U + u*G + lane (source chunks are consecutive across
+// the group's lanes, like the destination chunks); x[U] is the chunk after
+// the pass, loaded by the group's last lane only.  A misaligned piece also
+// needs the source chunk of clast.
+template <int G, int U>
+__device__ __forceinline__ void load_pass(__amdgpu_buffer_rsrc_t rs, const Piece &pc, uint32_t p, int lane,
+                                          uint32_t h, u32x4 (&x)[U + 1]) {
+  const uint32_t cb = pc.cfirst + p * (G * U);
+  const uint32_t lim = pc.clast + (((pc.del - h) & 15u) ? 1u : 0u);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint32_t ci = cb + u * G + lane;
+    x[u] = ld16(rs, ci < lim ? (16u * ci - h + pc.del) & ~15u : kOOB);
+  }
+  const uint32_t ci = cb + U * G;
+  x[U] = ld16(rs, lane == G - 1 && ci < lim ? (16u * ci - h + pc.del) & ~15u : kOOB);
+}
+// Destination chunk u of pass p, shifted into destination alignment (the
+// second source chunk is the next lane's, fetched with a DPP row shift) and
+// masked to the piece.
+template <int G, int U>
+__device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, const Piece &pc, uint32_t p,
+                                            int lane, uint32_t h) {
+  const uint32_t ci = pc.cfirst + p * (G * U) + u * G + lane;
+  const int cs = (int)(16u * ci) - (int)h;
+  const bool last = lane == G - 1;
+  // (computed by every lane before the select: a ternary arm is evaluated only
+  // by the lanes that take it, and the DPP would read switched-off lanes)
+  const u32x4 nl = next_lane4<G>(x[u], x[u + 1 < U ? u + 1 : u], last);
+  const u32x4 nx = u + 1 < U ? nl : (last ? x[U] : nl);
+  u32x4 v{0, 0, 0, 0};
+  if (ci < pc.clast) merge_bytes(v, shift2(x[u], nx, (uint32_t)cs + pc.del), pc.pa - cs, pc.pe - cs);
+  return v;
+}
+
+template <int G, int U>
+__global__ __launch_bounds__(kBlock, TX_WAVES) void k_tx_copy(TxDesc t) {
+  Desc ds{}, dd{};
+  ds.base = t.src;
+  ds.bytes = t.src_bytes;
+  dd.base = t.dst;
+  dd.bytes = t.dst_bytes;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t stride = gridDim.x * (kBlock / G);
+  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < t.n; i += stride) {
+    const uint32_t len = t.pkt_len[i];
+    const uint32_t k0 = t.pkt_seg[i], k1 = t.pkt_seg[i + 1];
+    const uint32_t nseg = k1 - k0;
+    const uint32_t l3 = t.l3;
+    const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
+    const uint32_t h = D & 15u, c0 = D & ~15u;
+    uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
+    // walk 1: bytes in the chain, the IP mbuf (segment holding frame byte l3)
+    // and its m_len from the IP header on
+    uint32_t total = 0, ip_mlen = 0, kip = 0;
+    for (uint32_t w = k0; w < k1 && !st; w += G) {
+      const uint32_t k = w + lane;
+      const uint32_t l = k < k1 ? (uint32_t)max(t.seg_len[k], 0) : 0u;
+      const uint32_t inc = group_scan<G>(l);
+      const uint32_t a = total + inc - l, e = total + inc;
+      const bool isip = l && a <= l3 && l3 < e;
+      ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
+      kip += group_sum<G>(isip ? k - k0 : 0u);
+      total += group_lane<G>(inc, G - 1);
+    }
+    if (!st && total < len) st = MI_TX_SHORT;
+#ifdef TX_DEBUG
+    if (i < 2) printf("i=%u lane=%d len=%u k0=%u k1=%u total=%u ip_mlen=%u kip=%u st=%u seglen=%d\n", i, lane, len, k0, k1, total, ip_mlen, kip, st, (int)(k0 + lane < k1 ? t.seg_len[k0 + lane] : -1));
+#endif
+    if (st) {
+      if (lane == 0) t.status[i] = (uint8_t)st;
+      continue;
+    }
+    ip_mlen = group_lane<G>(ip_mlen, 0);
+    kip = group_lane<G>(kip, 0);
+    const bool odd = (h + l3) & 1u;  // parity of the IP header's destination address
+    IpHdr ih{};
+    bool ok = false, do_ip = false, do_l4 = false, udp = false, done = false;
+    uint32_t at = 0;
+    int hend = 0, lend = 0;
+    uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
+    auto decide1 = [&](const u32x4 &h0, uint32_t hoff) {
+      const u32x4 hv[1] = {h0};
+      ih = parse_ipv4<G, 1>(hv, hoff);
+      const uint32_t flen = len >= l3 ? len - l3 : 0u;
+      ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl && ih.iplen <= flen;
+      const uint32_t fl = t.cflags ? t.cflags[i]
+                                   : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
+      do_ip = ok && (fl & MI_CSUM_IP);
+      do_l4 = ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
+      udp = fl & MI_CSUM_UDP;
+      at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? 16u : 6u);
+      hend = ok ? (int)ih.hl : 0;
+      lend = ok ? (int)ih.iplen : 0;
+    };
+    auto fold_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t p) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int rel = (int)(16u * (cfirst + p * (G * U) + u * G + lane)) - (int)(h + l3);
+        fold_chunk(v[u], rel, lend, hend, hend > 20, acc_t, acc_h, acc_f);
+      }
+    };
+    auto store_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t clast, uint32_t p, int pa, int pe,
+                         int u0 = 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (u < u0) continue;
+        const uint32_t ci = cfirst + p * (G * U) + u * G + lane;
+        const int cs = (int)(16u * ci) - (int)h;
+        if (ci < clast) store_chunk(rd, c0 + 16u * ci, v[u], pa - cs, pe - cs);
+      }
+    };
+    if (nseg <= (uint32_t)G && ip_mlen >= 20u) {
+      // ---- fast path: segment-major.  The IP mbuf's first chunks stay in
+      // registers (header parse, sum-field patches); every other chunk is
+      // gathered, folded and stored as it streams by.
+      const uint32_t k = k0 + lane;
+      const bool hs = (uint32_t)lane < nseg;
+      const int sl = hs ? max(t.seg_len[k], 0) : 0;
+      const uint32_t so = hs ? (uint32_t)t.seg_off[k] : 0u;
+      const int sa = (int)group_scan<G>((uint32_t)sl) - sl;
+      auto piece = [&](uint32_t j) {
+        Piece pc;
+        pc.pa = (int)group_lane<G>((uint32_t)sa, j);
+        pc.pe = min(pc.pa + (int)group_lane<G>((uint32_t)sl, j), (int)len);
+        pc.del = group_lane<G>(so, j) - (uint32_t)pc.pa;
+        pc.cfirst = (h + pc.pa) >> 4;
+        pc.clast = pc.pe > pc.pa ? (h + pc.pe + 15u) >> 4 : pc.cfirst;
+        return pc;
+      };
+      // stream pass p of piece pc: gather, fold, store (u >= u0)
+      auto stream = [&](const Piece &pc, uint32_t p, const u32x4 (&x)[U + 1], int u0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < u0) continue;
+          const u32x4 v = make_chunk<G, U>(x, u, pc, p, lane, h);
+          const uint32_t ci = pc.cfirst + p * (G * U) + u * G + lane;
+          const int cs = (int)(16u * ci) - (int)h;
+          fold_chunk(v, cs - (int)l3, lend, hend, hend > 20, acc_t, acc_h, acc_f);
+          if (ci < pc.clast) store_chunk(rd, c0 + 16u * ci, v, pc.pa - cs, pc.pe - cs);
+        }
+      };
+      const Piece ipc = piece(kip);
+      u32x4 held;
+      {
+        u32x4 x[U + 1];
+        load_pass<G, U>(rs, ipc, 0, lane, h, x);
+        u32x4 hv[1] = {make_chunk<G, U>(x, 0, ipc, 0, lane, h)};
+        decide1(hv[0], h + l3 - 16u * ipc.cfirst);
+        held = hv[0];
+        const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+        const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+        const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
+        done = (uint64_t)need + h <= 16ull * (ipc.cfirst + G);  // the patches land in held
+        if (done) {
+          fold_chunk(held, (int)(16u * (ipc.cfirst + lane)) - (int)(h + l3), lend, hend, hend > 20, acc_t,
+                     acc_h, acc_f);
+          stream(ipc, 0, x, 1);
+        }
+      }
+      if (done) {
+        for (uint32_t p = 1; p * (G * U) < ipc.clast - ipc.cfirst; ++p) {
+          u32x4 x[U + 1];
+          load_pass<G, U>(rs, ipc, p, lane, h, x);
+          stream(ipc, p, x, 0);
+        }
+        for (uint32_t j = 0; j < nseg; ++j) {
+          if (j == kip) continue;
+          const Piece pc = piece(j);
+          for (uint32_t p = 0; p * (G * U) < pc.clast - pc.cfirst; ++p) {
+            u32x4 x[U + 1];
+            load_pass<G, U>(rs, pc, p, lane, h, x);
+            stream(pc, p, x, 0);
+          }
+        }
+        const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+        uint32_t c_ip, c_l4;
+        tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
+        const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+        const int b0 = (int)h - (int)(16u * (ipc.cfirst + lane));  // frame offset -> byte of held
+        if (do_ip) {
+          if (pip < len) put_byte(held, (int)pip + b0, c_ip);
+          if (pip + 1u < len) put_byte(held, (int)pip + 1 + b0, c_ip >> 8);
+        }
+        if (l4_store) {
+          if (pl4 < len) put_byte(held, (int)pl4 + b0, c_l4);
+          if (pl4 + 1u < len) put_byte(held, (int)pl4 + 1 + b0, c_l4 >> 8);
+        }
+        const uint32_t ci = ipc.cfirst + lane;
+        const int cs = (int)(16u * ci) - (int)h;
+        if (ci < ipc.clast) store_chunk(rd, c0 + 16u * ci, held, ipc.pa - cs, ipc.pe - cs);
+        if (lane == 0)
+          t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+      }
+    }
+#ifndef TX_NO_GENERIC
+    if (!done) {
+      // ---- generic path (long chains, an IP header split over mbufs, sum
+      // fields far from the header): chunk-major over the whole frame, every
+      // piece of every chunk gathered by walking the chain; chunks stored as
+      // they are built, the sum fields patched once they have landed.
+      acc_t = acc_h = acc_f = 0;
+      const uint32_t nch = (h + len + 15u) >> 4;
+      const uint32_t npass = (nch + G * U - 1) / (G * U);
+      for (uint32_t p = 0; p < npass; ++p) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int cs = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
+          v[u] = u32x4{0, 0, 0, 0};
+          int pos = 0;
+          for (uint32_t k = k0; k < k1; ++k) {
+            const int l = max(t.seg_len[k], 0);
+            const int lo = max(pos - cs, 0), hi = min(min(pos + l, (int)len) - cs, 16);
+            if (hi > lo) {
+              const uint32_t a = (uint32_t)cs + ((uint32_t)t.seg_off[k] - (uint32_t)pos);
+              merge_bytes(v[u], shift_pair(ld_pair(rs, a), a), lo, hi);
+            }
+            pos += l;
+          }
+        }
+        if (p == 0) decide1(v[0], h + l3);
+        fold_all(v, 0, p);
+        store_all(v, 0, nch, p, 0, (int)len);
+      }
+      if (npass == 0) ok = do_ip = do_l4 = false;
+      const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+      uint32_t c_ip, c_l4;
+      tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
+      if (do_ip || l4_store) {
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's chunk stores have landed
+        if (lane == 0) {
+          const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+          if (do_ip) {
+            if (pip < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_ip, rd, D + pip, 0, 0);
+            if (pip + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_ip >> 8), rd, D + pip + 1u, 0, 0);
+          }
+          if (l4_store) {
+            if (pl4 < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_l4, rd, D + pl4, 0, 0);
+            if (pl4 + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_l4 >> 8), rd, D + pl4 + 1u, 0, 0);
+          }
+        }
+      }
+      if (lane == 0)
+        t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+    }
+#endif
+  }
+}
+
 // Scalar drop-in path: one span in page-locked host memory (read over PCIe).
 __global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
                                                uint32_t len, uint32_t abs_lanes, int pseudo,
@@ -1174,6 +1635,42 @@ int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
   return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
 }
 
+// TX copy shapes: G = 8 or 16 (row-local DPP neighbour exchange; the IP
+// header sits in the u = 0 chunks of lanes 0..G-1).  Long pieces loop over
+// passes of G*U chunks.
+#define FOR_TX_GU(X) X(8, 2) X(8, 4) X(8, 8) X(16, 2) X(16, 4) X(16, 6) X(16, 8)
+
+Shape pick_tx_shape(uint32_t max_len) {
+  static const Shape forced = [] {
+    Shape f{0, 0};
+    if (const char *e = getenv("MI_CKSUM_TX_SHAPE")) {
+      int g = 0, u = 0;
+      if (sscanf(e, "%dx%d", &g, &u) == 2) f = {g, u};
+    }
+    return f;
+  }();
+  if (forced.g) return forced;
+  // mi_cksum_set_shape applies when it names a TX shape
+#define X(G_, U_) if (g_tune.g == G_ && g_tune.u == U_) return {G_, U_};
+  FOR_TX_GU(X)
+#undef X
+  const uint32_t ch = (max_len + 15u + 15u) / 16u;
+  if (ch <= 32) return {8, 4};
+  return {16, 6};
+}
+
+int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
+  const int grid = grid_for(t.n, sh.g);
+#define X(G_, U_)                                                                  \
+  if (sh.g == G_ && sh.u == U_) {                                                  \
+    hipLaunchKernelGGL((k_tx_copy<G_, U_>), dim3(grid), dim3(kBlock), 0, s, t);    \
+    return launched();                                                             \
+  }
+  FOR_TX_GU(X)
+#undef X
+  return set_err(-EINVAL, "no TX kernel for shape %dx%d", sh.g, sh.u);
+}
+
 }  // namespace
 
 // ====================================================================== C ABI
@@ -1370,6 +1867,41 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
   }
   if (span_us) *span_us = span * 1000.f;
   return 0;
+}
+
+int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (!b->n) return 0;
+  if (!b->src || !b->dst || !b->seg_off || !b->seg_len || !b->pkt_seg || !b->pkt_len || !status)
+    return set_err(-EINVAL, "NULL array");
+  if (((uintptr_t)b->src & 15u) || ((uintptr_t)b->dst & 15u))
+    return set_err(-EINVAL, "src / dst not 16-byte aligned");
+  if (b->src_bytes > kMaxBytes || b->dst_bytes > kMaxBytes) return set_err(-E2BIG, "buffer >= 4 GiB");
+  if (b->l3_off > 64) return set_err(-EINVAL, "l3_off %u > 64", b->l3_off);
+  const uint64_t last = b->dst_first + (uint64_t)(b->n - 1) * b->dst_stride + b->room;
+  if (last > b->dst_bytes)
+    return set_err(-ERANGE, "slot %u ends at %llu > dst_bytes %llu", b->n - 1, (unsigned long long)last,
+                   (unsigned long long)b->dst_bytes);
+  TxDesc t{};
+  t.src = (const uint8_t *)b->src;
+  t.src_bytes = (uint32_t)((b->src_bytes + 15u) & ~15ull);
+  t.n = b->n;
+  t.seg_off = b->seg_off;
+  t.seg_len = b->seg_len;
+  t.pkt_seg = b->pkt_seg;
+  t.pkt_len = b->pkt_len;
+  t.cflags = b->csum_flags;
+  t.cdata = b->csum_data;
+  t.dst = (uint8_t *)b->dst;
+  t.dst_bytes = (uint32_t)b->dst_bytes;
+  t.room = b->room;
+  t.l3 = b->l3_off;
+  t.dst_stride = b->dst_stride;
+  t.dst_first = b->dst_first;
+  t.status = status;
+  return launch_tx(t, pick_tx_shape(b->max_len ? b->max_len : b->room), (hipStream_t)stream);
 }
 
 int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {

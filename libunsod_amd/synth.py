@@ -141,3 +141,80 @@ def packed_offsets(lengths: np.ndarray, first_off: int = 0, align: int = 8) -> n
     if len(sz):
         o[1:] = np.cumsum(sz)[:-1]
     return (o + first_off).astype(np.uint64)
+
+
+# ------------------------------------------------------------- TX mbuf chains
+MSIZE = 256           # param.h:159
+MHLEN_OFF = 56        # m_pktdat inside a packet-header mbuf (MSIZE - MHLEN, mbuf.h)
+MCLBYTES = 2048       # param.h
+
+
+def build_tx_chains(n: int, ip_len, *, layout: str = "socket", proto=IPPROTO_TCP, hl=20,
+                    seed: int = 0x7E57, l3_off: int = ETH_HLEN) -> dict:
+    """``n`` outgoing Ethernet frames as mbuf chains in one source blob, with
+    the sums still to be done (ip_sum = 0, L4 field = in_pseudo seed), as
+    ip_output hands them to the driver under if_hwassist (ip_output.c:649-672).
+
+    layout:
+      "socket" -- what tcp_output builds (tcp_output.c:848-900): a header mbuf
+                  (256 B, data near its end after M_PREPEND of the link header)
+                  holding Ethernet + IP + TCP headers, then the payload as
+                  references into 2 KiB socket-buffer clusters at a running
+                  offset (1 or 2 pieces per frame);
+      "single" -- the whole frame in one cluster (m_data 16-aligned + 2);
+      "random" -- random cut points (zero-length mbufs, 1-byte mbufs, the IP
+                  header split across mbufs) at random addresses mod 64.
+    Returns dict(src, seg_off, seg_len, pkt_seg, pkt_len, frames) -- ``frames``
+    are the contiguous frame bytes (what m_copydata yields).
+    """
+    rng = np.random.default_rng(seed)
+    L = np.broadcast_to(np.asarray(ip_len, np.int64), (n,)).copy()
+    dg = build_ipv4_batch(n, L, stride=int(L.max()) + 64, first_off=0, proto=proto, hl=hl, seed=seed)
+    frames = []
+    for i in range(n):
+        o = int(dg["offs"][i])
+        eth = bytes([0x02, 0, 0, 0, 0, 1, 0x02, 0, 0, 0, 0, 2, 0x08, 0x00])[:l3_off].ljust(l3_off, b"\0")
+        frames.append(eth + dg["buf"][o:o + int(L[i])].tobytes())
+    blob = bytearray()
+    seg_off, seg_len, pkt_seg = [], [], [0]
+
+    def put(data: bytes, addr_mod: int, align: int = 64):
+        pad = (addr_mod - len(blob)) % align
+        blob.extend(b"\0" * pad)
+        seg_off.append(len(blob))
+        seg_len.append(len(data))
+        blob.extend(data)
+
+    sb_off = 0  # running offset in the socket buffer's clusters
+    for i, fr in enumerate(frames):
+        hdr_len = l3_off + (int(np.broadcast_to(hl, (n,))[i])) + (20 if int(np.broadcast_to(proto, (n,))[i]) == IPPROTO_TCP else 8)
+        if layout == "socket":
+            hdr_len = min(hdr_len, len(fr))
+            put(fr[:hdr_len], (MSIZE - 16 - hdr_len) % 64)  # header mbuf: data ends near m_dat's end
+            pay = fr[hdr_len:]
+            while pay:
+                room = MCLBYTES - sb_off % MCLBYTES
+                take = min(room, len(pay))
+                put(pay[:take], sb_off % MCLBYTES % 64)
+                pay = pay[take:]
+                sb_off += take
+        elif layout == "single":
+            put(fr, 2)
+        elif layout == "random":
+            cuts = sorted(set(int(c) for c in rng.integers(0, len(fr) + 1, int(rng.integers(0, 6)))))
+            if rng.random() < 0.3:  # split the IP header
+                cuts.append(l3_off + int(rng.integers(1, 20)))
+            cuts = sorted(c for c in set(cuts) if 0 <= c <= len(fr))
+            prev = 0
+            for c in cuts + [len(fr)]:
+                put(fr[prev:c], int(rng.integers(0, 64)))
+                if rng.random() < 0.1:
+                    put(b"", int(rng.integers(0, 64)))  # zero-length mbuf
+                prev = c
+        else:
+            raise ValueError(layout)
+        pkt_seg.append(len(seg_off))
+    blob.extend(b"\0" * (64 + (-len(blob)) % 64))
+    return dict(src=np.frombuffer(bytes(blob), np.uint8).copy(), seg_off=np.array(seg_off, np.uint64),
+                seg_len=np.array(seg_len, np.int32), pkt_seg=np.array(pkt_seg, np.uint32),
+                pkt_len=np.array([len(f) for f in frames], np.uint32), frames=frames)

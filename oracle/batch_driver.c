@@ -237,3 +237,127 @@ uint16_t F(chain_pseudo)(const uint8_t *const *seg, const int32_t *seglen,
 	build_chain(mb, seg, seglen, nseg);
 	return F(in_cksum_pseudo_header)(&mb[0].m, plen, off0, src, dst, proto);
 }
+
+/*
+ * TX with checksum offload, restated as the software path the device must
+ * match byte for byte (see oracle.h).  Frame i is the
+ * chain of segments [pkt_seg[i], pkt_seg[i+1]) (seg_off/seg_len into src =
+ * m_data/m_len), pkt_len[i] bytes (m_pkthdr.len), IP header l3_off bytes in.
+ *   len > room                        -> NOBUFS, nothing written  (uinet_if_dpdk.c:585-591)
+ *   chain holds < len bytes           -> SHORT, nothing written   (m_copydata's KASSERT)
+ *   m_copydata(m, 0, len, dst)                                     (uinet_if_dpdk.c:597)
+ *   IP datagram malformed (finalize rules, flen = len - l3_off)    -> NOSUM, the copy stays
+ *   flags & (CSUM_TCP|CSUM_UDP): in_delayed_cksum (ip_output.c:958-983) on the
+ *       chain from the IP header: c = in_cksum_skip(m, ip_len, hl), CSUM_UDP 0 -> 0xffff,
+ *       stored at hl + csum_data iff those 2 bytes lie inside the IP mbuf's m_len
+ *       (else L4_SKIPPED: the "delayed m_pullup" printf, :971-981)
+ *   flags & CSUM_IP: ip_sum = 0; ip_sum = in_cksum(m, hl)          (ip_output.c:667-672)
+ * The sums are taken before the copy in the stack; only bytes inside the
+ * frame's len reach the wire, so stores past len are dropped.  "The IP mbuf"
+ * is the segment holding frame byte l3_off, from that byte on.  The chain the
+ * sums walk is rebuilt over the copied bytes with the source's segmentation
+ * (in_cksum_skip's result does not depend on where the bytes sit, only on the
+ * walk), so the reference's chain walk runs on every case.
+ */
+static uint32_t tx_default_flags(uint8_t proto)
+{
+	return ORC_CSUM_IP | (proto == 6 ? ORC_CSUM_TCP : proto == 17 ? ORC_CSUM_UDP : 0u);
+}
+
+void F(tx_copy_batch)(const uint8_t *src, const uint64_t *seg_off,
+    const int32_t *seg_len, const uint32_t *pkt_seg, const uint32_t *pkt_len,
+    const uint32_t *csum_flags, const uint32_t *csum_data, uint32_t l3_off,
+    uint8_t *dst, uint64_t dst_stride, uint64_t dst_first, uint32_t room,
+    uint32_t n, uint8_t *status)
+{
+	for (uint32_t i = 0; i < n; i++) {
+		const uint32_t k0 = pkt_seg[i], k1 = pkt_seg[i + 1];
+		const uint32_t len = pkt_len[i];
+		uint8_t *fr = dst + dst_first + (uint64_t)i * dst_stride;
+		uint8_t st = 0;
+		uint64_t total = 0, pos = 0;
+		int64_t ip_mlen = -1;
+		uint32_t nseg = 0;
+		union drv_mbuf mb[MAX_SEGS];
+		if (len > room) {
+			status[i] = ORC_TX_NOBUFS;
+			continue;
+		}
+		for (uint32_t k = k0; k < k1; k++)
+			total += seg_len[k] > 0 ? (uint64_t)seg_len[k] : 0;
+		if (total < len) {
+			status[i] = ORC_TX_SHORT;
+			continue;
+		}
+		/* m_copydata(m, 0, len, fr) */
+		for (uint32_t k = k0; k < k1 && pos < len; k++) {
+			uint64_t l = seg_len[k] > 0 ? (uint64_t)seg_len[k] : 0;
+			if (l > len - pos)
+				l = len - pos;
+			memcpy(fr + pos, src + seg_off[k], l);
+			pos += l;
+		}
+		/* the IP datagram's chain over the copy, source segmentation */
+		pos = 0;
+		for (uint32_t k = k0; k < k1 && pos < len; k++) {
+			uint64_t l = seg_len[k] > 0 ? (uint64_t)seg_len[k] : 0;
+			uint64_t a = pos, e = pos + l;
+			pos = e;
+			if (e <= l3_off)
+				continue;
+			if (a < l3_off) {
+				ip_mlen = (int64_t)(e - l3_off);
+				a = l3_off;
+			} else if (ip_mlen < 0) {
+				ip_mlen = (int64_t)l;
+			}
+			if (e > len)
+				e = len;
+			if (nseg < MAX_SEGS) {
+				memset(&mb[nseg], 0, sizeof(mb[nseg]));
+				mb[nseg].m.m_data = (char *)(fr + a);
+				mb[nseg].m.m_len = (int32_t)(e - a);
+				if (nseg)
+					mb[nseg - 1].m.m_next = &mb[nseg].m;
+				nseg++;
+			}
+		}
+		{
+			const uint32_t flen = len >= l3_off ? len - l3_off : 0;
+			uint8_t *ip = fr + l3_off;
+			uint32_t hl = 0, iplen = 0, fl, at;
+			if (flen >= 20) {
+				hl = (uint32_t)(ip[0] & 0x0f) << 2;
+				iplen = ((uint32_t)ip[2] << 8) | ip[3];
+			}
+			if (flen < 20 || hl < 20 || hl > flen || iplen < hl || iplen > flen || !nseg) {
+				status[i] = ORC_TX_NOSUM;
+				continue;
+			}
+			fl = csum_flags ? csum_flags[i] : tx_default_flags(ip[9]);
+			if (fl & (ORC_CSUM_TCP | ORC_CSUM_UDP)) {
+				uint16_t c = F(in_cksum_skip)(&mb[0].m, (int)iplen, (int)hl);
+				uint32_t cd = csum_data ? csum_data[i] : (fl & ORC_CSUM_TCP) ? 16u : 6u;
+				if ((fl & ORC_CSUM_UDP) && c == 0)
+					c = 0xffff;
+				at = hl + cd;
+				if ((uint64_t)at + 2 > (uint64_t)ip_mlen) {
+					st |= ORC_TX_L4_SKIPPED;
+				} else {
+					/* *(u_short *)(m_data + at) = c, of which the bytes inside len reach the wire */
+					if ((uint64_t)l3_off + at < len)
+						ip[at] = (uint8_t)c;
+					if ((uint64_t)l3_off + at + 1 < len)
+						ip[at + 1] = (uint8_t)(c >> 8);
+				}
+			}
+			if (fl & ORC_CSUM_IP) {
+				uint16_t c;
+				ip[10] = ip[11] = 0;
+				c = F(in_cksum_skip)(&mb[0].m, (int)hl, 0);
+				memcpy(ip + 10, &c, 2);
+			}
+		}
+		status[i] = st;
+	}
+}

@@ -77,6 +77,21 @@ uint16_t orc_in_addword(uint16_t a, uint16_t b);
 #define ORC_ST_L4_BAD    2u
 #define ORC_ST_MALFORMED 4u
 
+/*
+ * tx_copy_batch (TX checksum offload fused with the driver's copy,
+ * uinet_if_dpdk.c:561-606 + ip_output.c:649-672,958-983): see batch_driver.c.
+ * csum_flags (m_pkthdr.csum_flags, mbuf.h:281-288; NULL -> CSUM_IP plus
+ * CSUM_TCP / CSUM_UDP by ip_p) and csum_data (offset of the L4 sum field, NULL
+ * -> 16 TCP / 6 UDP, tcp_output.c:1066, udp_usrreq.c:1240).
+ */
+#define ORC_CSUM_IP  0x1u
+#define ORC_CSUM_TCP 0x2u
+#define ORC_CSUM_UDP 0x4u
+#define ORC_TX_NOBUFS     1u
+#define ORC_TX_SHORT      2u
+#define ORC_TX_NOSUM      4u
+#define ORC_TX_L4_SKIPPED 8u
+
 #define ORC_DECL_BATCH(PFX)                                                     \
 	void PFX##ipv4_verify_batch(const uint8_t *base, const uint64_t *offs,     \
 	    uint64_t stride, uint64_t first_off, const uint32_t *flen,              \
@@ -90,7 +105,13 @@ uint16_t orc_in_addword(uint16_t a, uint16_t b);
 	    int nseg, int len, int skip);                                           \
 	uint16_t PFX##chain_pseudo(const uint8_t *const *seg,                       \
 	    const int32_t *seglen, int nseg, int plen, int off0, uint32_t src,      \
-	    uint32_t dst, uint8_t proto);
+	    uint32_t dst, uint8_t proto);                                           \
+	void PFX##tx_copy_batch(const uint8_t *src, const uint64_t *seg_off,       \
+	    const int32_t *seg_len, const uint32_t *pkt_seg,                        \
+	    const uint32_t *pkt_len, const uint32_t *csum_flags,                    \
+	    const uint32_t *csum_data, uint32_t l3_off, uint8_t *dst,               \
+	    uint64_t dst_stride, uint64_t dst_first, uint32_t room, uint32_t n,     \
+	    uint8_t *status);
 
 ORC_DECL_BATCH(orc_)
 ORC_DECL_BATCH(ref_)

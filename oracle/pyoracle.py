@@ -91,6 +91,9 @@ class Oracle:
                                 C.c_uint32, C.c_int]
         self._repeat = g("skip_repeat"); self._repeat.restype = C.c_uint64
         self._repeat.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        self._tx = g("tx_copy_batch"); self._tx.restype = None
+        self._tx.argtypes = [C.c_void_p, u64p, C.POINTER(C.c_int32), u32p, u32p, u32p, u32p, C.c_uint32,
+                             C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, u8p]
 
     # --- scalar reference entry points (in_cksum.h:77-83) -------------------
     def in_pseudo(self, a: int, b: int, c: int) -> int:
@@ -148,6 +151,31 @@ class Oracle:
 
     def skip_repeat(self, buf: np.ndarray, length: int, iters: int) -> int:
         return int(self._repeat(buf.ctypes.data, length, iters))
+
+    def tx_copy_batch(self, src: np.ndarray, seg_off, seg_len, pkt_seg, pkt_len, dst: np.ndarray, *,
+                      dst_stride: int, dst_first: int, room: int, l3_off: int = 14, csum_flags=None,
+                      csum_data=None) -> np.ndarray:
+        """TX offload fused with the driver's copy (batch_driver.c tx_copy_batch):
+        frame i = chain of segments [pkt_seg[i], pkt_seg[i+1]) of ``src`` copied
+        into ``dst`` at dst_first + i*dst_stride with in_delayed_cksum / ip_sum
+        applied as the software stack would.  ``dst`` is written in place;
+        returns the per-frame status (ORC_TX_* bits)."""
+        seg_off = np.ascontiguousarray(seg_off, np.uint64)
+        seg_len = np.ascontiguousarray(seg_len, np.int32)
+        pkt_seg = np.ascontiguousarray(pkt_seg, np.uint32)
+        pkt_len = np.ascontiguousarray(pkt_len, np.uint32)
+        n = len(pkt_len)
+        cf = None if csum_flags is None else np.ascontiguousarray(csum_flags, np.uint32)
+        cd = None if csum_data is None else np.ascontiguousarray(csum_data, np.uint32)
+        st = np.zeros(n, np.uint8)
+        self._tx(src.ctypes.data, _ptr(seg_off, u64p), seg_len.ctypes.data_as(C.POINTER(C.c_int32)),
+                 _ptr(pkt_seg, u32p), _ptr(pkt_len, u32p), _ptr(cf, u32p), _ptr(cd, u32p), l3_off,
+                 dst.ctypes.data, dst_stride, dst_first, room, n, _ptr(st, u8p))
+        return st
+
+
+TX_NOBUFS, TX_SHORT, TX_NOSUM, TX_L4_SKIPPED = 1, 2, 4, 8
+CSUM_IP, CSUM_TCP, CSUM_UDP = 0x1, 0x2, 0x4  # mbuf.h:281-283
 
 
 # --- RX offload flags (SURVEY.md 8(f) rank 1) -----------------------------------
