@@ -116,6 +116,12 @@ typedef struct mi_pkt_batch {
 } mi_pkt_batch;
 
 #define MI_BATCH_PACKED 1u
+/* MI_BATCH_DEMUX: verify / finalize take each datagram's L4 checksum the way
+ * ip_input's protocol switch hands it on (the
+ * small-header callers): TCP / UDP with the pseudo header, ICMP / IGMP / CARP
+ * plain in_cksum, fragments and other protocols none.  See
+ * mi_cksum_ipv4_verify and mi_cksum_ipv4_finalize. */
+#define MI_BATCH_DEMUX  2u
 
 /* Lane conventions for mi_cksum_span_batch. */
 #define MI_SPAN_STREAM 0u  /* in_cksum_skip / in_cksum_pseudo_header: lanes
@@ -181,6 +187,7 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);
 #define MI_ST_IP_BAD    1u
 #define MI_ST_L4_BAD    2u
 #define MI_ST_MALFORMED 4u
+#define MI_ST_L4_NONE   8u  /* MI_BATCH_DEMUX: no L4 checksum applies */
 
 /*
  * RX verify of IPv4 datagrams (ip_input.c:459-471 + tcp_input.c:697-720 /
@@ -191,8 +198,26 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);
  *   ip = (hl == 20) ? in_cksum_hdr(ip) : in_cksum(m, hl)
  *   ip_len < hl || ip_len > flen       -> l4 = 0, MALFORMED
  *   else l4 = in_cksum_pseudo_header(m, ip_len - hl, hl, ip_src, ip_dst, ip_p)
+ * With MI_BATCH_DEMUX in b->flags, l4 is instead what the protocol's input
+ * routine tests (0 = accept), plen = ip_len - hl, the mbuf trimmed to ip_len
+ * (ip_input.c:500-505):
+ *   fragment (IP_MF or an offset)       -> l4 = 0, L4_NONE (summed after ip_reass)
+ *   TCP  plen < 20 -> MALFORMED (tcps_rcvshort, tcp_input.c:688-693); else as above
+ *   UDP  plen < 8 -> MALFORMED (udps_hdrops, udp_usrreq.c:375-381);
+ *        uh_ulen > plen or < 8 -> MALFORMED (udps_badlen, :406-414), shorter
+ *        -> trimmed to uh_ulen; uh_sum == 0 -> L4_NONE (udps_nosum, :429,451);
+ *        else in_cksum_pseudo_header(m, uh_ulen, hl, src, dst, 17)   (:440-442)
+ *   ICMP plen < 36 -> MALFORMED (the pullup to hl + min(icmplen,
+ *        ICMP_ADVLENMIN) with icmplen = ntohs(ip_len), ip_icmp.c:336,374-378);
+ *        else in_cksum(m + hl, ip_len), which the trimmed chain truncates to
+ *        the plen ICMP bytes (ip_icmp.c:381-383)
+ *   IGMP plen < 8 -> MALFORMED (igps_rcv_tooshort, igmp.c:1445-1452);
+ *        else in_cksum(m + hl, plen)                                 (:1475-1478)
+ *   CARP (112) plen < 36 -> MALFORMED (carps_badlen, ip_carp.c:600-607);
+ *        else in_cksum(m + hl, 36) -- the header only                (:641-643)
+ *   other protocols                     -> l4 = 0, L4_NONE
  * Any output pointer may be NULL.  bad_count (device u32, may be NULL) gains
- * one per packet with a nonzero status.
+ * one per packet with a nonzero status other than L4_NONE alone.
  */
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                          uint8_t *status, uint32_t *bad_count, void *stream);
@@ -252,6 +277,14 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
  * (UDP: 0 -> 0xffff) stored at hl + (TCP 16 | UDP 6) when inside lens[i]; then
  * ip_sum = in_cksum(m, hl) with the ip_sum field taken as 0.  Malformed
  * datagrams (as above) are left untouched.
+ * With MI_BATCH_DEMUX: fragments get ip_sum only (ip_fragment sums the whole
+ * datagram before cutting it and each piece's header after, ip_output.c:
+ * 930,950); TCP / UDP as above; the small-header senders store a plain
+ * in_cksum over their message with the sum field taken as 0:
+ *   ICMP plen >= 8:  icmp_cksum at hl + 2 over plen bytes    (ip_icmp.c:889-891)
+ *   IGMP plen >= 8:  igmp_cksum at hl + 2 over plen bytes    (igmp.c:2184-2185, :3483)
+ *   CARP plen >= 36: carp_cksum at hl + 6 over 36 bytes      (ip_carp.c:944,985)
+ * other protocols: ip_sum only.
  */
 int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream);
 

@@ -5,7 +5,7 @@ The product is the C-ABI library ``lib/libmicksum.so`` (HIP kernels for gfx950
 (and raises if it is missing: there is no CPU fallback) and mirrors the
 reference interface in Python for tests and the bench.
 """
-from ._lib import (LIB_PATH, MI_SPAN_ABS, MI_SPAN_STREAM, MI_ST_IP_BAD, MI_ST_L4_BAD, MI_ST_MALFORMED,
+from ._lib import (LIB_PATH, MI_SPAN_ABS, MI_SPAN_STREAM, MI_ST_IP_BAD, MI_ST_L4_BAD, MI_ST_MALFORMED, MI_ST_L4_NONE,
                    MiCksumError, load)
 from .api import (ChainBatch, MbufChain, chain_batch, PktBatch, device_count, host_register, host_unregister, in_addword, in_cksum,
                   in_cksum_hdr, in_cksum_pseudo_header, in_cksum_skip, in_pseudo, init, ipv4_finalize,
@@ -15,7 +15,7 @@ from .api import (ChainBatch, MbufChain, chain_batch, PktBatch, device_count, ho
 load()
 
 __all__ = [
-    "LIB_PATH", "MI_SPAN_ABS", "MI_SPAN_STREAM", "MI_ST_IP_BAD", "MI_ST_L4_BAD", "MI_ST_MALFORMED",
+    "LIB_PATH", "MI_SPAN_ABS", "MI_SPAN_STREAM", "MI_ST_IP_BAD", "MI_ST_L4_BAD", "MI_ST_MALFORMED", "MI_ST_L4_NONE",
     "MiCksumError", "load", "ChainBatch", "MbufChain", "chain_batch", "PktBatch", "device_count", "host_register", "host_unregister",
     "in_addword", "in_cksum", "in_cksum_hdr", "in_cksum_pseudo_header", "in_cksum_skip", "in_pseudo", "init",
     "ipv4_finalize", "ipv4_verify", "ipv4_verify_host", "ipv4_verify_repeat", "rx_offload", "span_batch", "verify_plan", "synth_ipv4", "version",

@@ -18,7 +18,9 @@ MI_SPAN_ABS = 1
 MI_ST_IP_BAD = 1
 MI_ST_L4_BAD = 2
 MI_ST_MALFORMED = 4
+MI_ST_L4_NONE = 8
 MI_BATCH_PACKED = 1
+MI_BATCH_DEMUX = 2
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2

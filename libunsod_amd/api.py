@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -103,11 +103,14 @@ class PktBatch:
     Packet i starts at ``offs[i]`` (device int64 tensor) or
     ``first_off + i*stride`` and is ``lens[i]`` (device int32 tensor) or
     ``fixed_len`` bytes long.  ``packed``: offsets ascend and datagrams sit back
-    to back (MI_BATCH_PACKED hint; correct either way).
+    to back (MI_BATCH_PACKED hint; correct either way).  ``demux``: verify /
+    finalize take each datagram's L4 sum the way ip_input's protocol switch
+    hands it on -- TCP / UDP / ICMP / IGMP / CARP, fragments none
+    (MI_BATCH_DEMUX, include/mi_cksum.h).
     """
 
     def __init__(self, buf, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
-                 fixed_len: int = 0, max_len: int = 0, packed: bool = False):
+                 fixed_len: int = 0, max_len: int = 0, packed: bool = False, demux: bool = False):
         torch = _torch()
         if buf.dtype != torch.uint8 or not buf.is_contiguous():
             raise ValueError("buf must be a contiguous uint8 tensor")
@@ -122,7 +125,8 @@ class PktBatch:
                             self.offs.data_ptr() if self.offs is not None else None,
                             self.stride, self.first_off,
                             self.lens.data_ptr() if self.lens is not None else None,
-                            self.fixed_len, self.n, self.max_len, MI_BATCH_PACKED if packed else 0)
+                            self.fixed_len, self.n, self.max_len,
+                            (MI_BATCH_PACKED if packed else 0) | (MI_BATCH_DEMUX if demux else 0))
 
     @property
     def c(self) -> PktBatchC:

@@ -295,7 +295,8 @@ __device__ __forceinline__ void fold_pass(const u32x4 (&v)[U], uint32_t p, int l
 template <int G, int U, bool TX>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                           int lane, u32x4 (&v)[U], IpHdr &ih, bool &hdr_ok,
-                                          bool &l4_ok, uint32_t &sum_h, uint32_t &sum_l) {
+                                          bool &l4_ok, uint32_t &sum_h, uint32_t &sum_l,
+                                          bool demux = false) {
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = (h + flen + 15u) >> 4;
   const uint32_t npass = (nch + G * U - 1) / (G * U);
@@ -303,7 +304,11 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   const bool odd = h & 1u;  // base is 16-byte aligned
   hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
   const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-  l4_ok = TX ? len_ok && (ih.proto == 6u || ih.proto == 17u) : len_ok;
+  // TX: the protocols whose senders sum their message (TCP / UDP; with
+  // MI_BATCH_DEMUX also ICMP, IGMP, CARP)
+  l4_ok = TX ? len_ok && (ih.proto == 6u || ih.proto == 17u ||
+                          (demux && (ih.proto == 1u || ih.proto == 2u || ih.proto == 112u)))
+             : len_ok;
   const int hend = hdr_ok && (!TX || len_ok) ? (int)ih.hl : 0;
   const int lend = l4_ok ? (int)ih.iplen : hend;
   const bool opts = hend > 20;  // group-uniform
@@ -452,6 +457,84 @@ __device__ __forceinline__ void rx_offload_store(const Desc &d, __amdgpu_buffer_
   if (d.cdata) d.cdata[i] = cd;
 }
 
+// ---- small-header callers (MI_BATCH_DEMUX).  Rare
+// per-datagram work done by one lane after the datagram's single pass: the
+// bytes it re-reads were just streamed, so they come from L2.
+
+// Absolute-lane sum of bytes [a, b) of the datagram at off.
+__device__ __forceinline__ uint32_t dgram_range(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t a,
+                                                uint32_t b) {
+  uint32_t s = 0;
+  for (uint32_t c = (off + a) & ~15u; c < off + b; c += 16u)
+    s += range_sum(__builtin_amdgcn_raw_buffer_load_b128(r, c, 0, 0), (int)(c - off), (int)a, (int)b);
+  return s;
+}
+__device__ __forceinline__ uint32_t ld_byte(__amdgpu_buffer_rsrc_t r, uint32_t o) {
+  return __builtin_amdgcn_raw_buffer_load_b8(r, o, 0, 0);
+}
+__device__ __forceinline__ uint32_t ld_be16(__amdgpu_buffer_rsrc_t r, uint32_t o) {
+  return (ld_byte(r, o) << 8) | ld_byte(r, o + 1u);
+}
+// Absolute-lane sum of the span [hl, hl + span) given S = sum of [hl, ip_len):
+// whichever of the span or the rest is shorter is re-read (S is exact, < 2^31).
+__device__ __forceinline__ uint32_t l4_span_sum(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
+                                                uint32_t span, uint32_t S) {
+  const uint32_t plen = ih.iplen - ih.hl;
+  if (span >= plen) return S;
+  if (span <= plen - span) return dgram_range(r, off, ih.hl, ih.hl + span);
+  return S - dgram_range(r, off, ih.hl + span, ih.iplen);
+}
+
+// RX: the L4 value the protocol input routine tests (mi_cksum.h, MI_BATCH_DEMUX).
+__device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
+                                         bool odd, uint32_t sum_l, uint32_t &l4, uint32_t &st) {
+  const uint32_t plen = ih.iplen - ih.hl;
+  const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
+  uint32_t need = 0, span = plen;
+  bool none = (ip_off & 0x3fffu) != 0u, pseudo = false;  // IP_MF | IP_OFFMASK: ip_reass first
+  if (!none) {
+    switch (ih.proto) {
+      case 6u: need = 20u; pseudo = true; break;    // tcp_input.c:688-693
+      case 17u: need = 8u; pseudo = true; break;    // udp_usrreq.c:375-381
+      case 1u: need = 36u; break;                   // ip_icmp.c:374-378
+      case 2u: need = 8u; break;                    // igmp.c:1448-1452
+      case 112u: need = 36u; span = 36u; break;     // ip_carp.c:600-607, :641-643
+      default: none = true;
+    }
+  }
+  l4 = 0;
+  if (none) {
+    st |= MI_ST_L4_NONE;
+    return;
+  }
+  if (plen < need) {
+    st |= MI_ST_MALFORMED;
+    return;
+  }
+  if (ih.proto == 17u) {
+    const uint32_t ulen = ld_be16(r, off + ih.hl + 4u);  // udp_usrreq.c:406-414
+    if (ulen != plen) {
+      if (ulen > plen || ulen < 8u) {
+        st |= MI_ST_MALFORMED;
+        return;
+      }
+      span = ulen;  // m_adj to uh_ulen
+    }
+    if (ld_be16(r, off + ih.hl + 6u) == 0u) {  // uh_sum == 0: udps_nosum
+      st |= MI_ST_L4_NONE;
+      return;
+    }
+  }
+  uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l));
+  if (odd) sl = swap16(sl);
+  if (pseudo) {
+    const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(span);
+    l4 = ~fold16_64(seed + sl) & 0xffffu;
+  } else {
+    l4 = ~sl & 0xffffu;
+  }
+}
+
 __device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok,
                                              bool l4_ok, uint32_t sum_h, uint32_t sum_l,
                                              uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
@@ -464,21 +547,23 @@ __device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &
     uint32_t sh = fold16(sum_h);
     if (ih.hl != 20u && odd) sh = swap16(sh);  // in_cksum (stream) vs in_cksum_hdr (abs)
     ip = ~sh & 0xffffu;
-    if (l4_ok) {
+    if (!l4_ok) {
+      st = MI_ST_MALFORMED;
+    } else if (d.flags & MI_BATCH_DEMUX) {
+      demux_l4(r, off, ih, odd, sum_l, l4, st);
+    } else {
       uint32_t sl = fold16(sum_l);
       if (odd) sl = swap16(sl);
       const uint32_t plen = ih.iplen - ih.hl;
       const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(plen);
       l4 = ~fold16_64(seed + sl) & 0xffffu;
-    } else {
-      st = MI_ST_MALFORMED;
     }
     st |= (ip ? MI_ST_IP_BAD : 0u) | (l4 ? MI_ST_L4_BAD : 0u);
   }
   if (ip_out) ip_out[i] = (uint16_t)ip;
   if (l4_out) l4_out[i] = (uint16_t)l4;
   if (st_out) st_out[i] = (uint8_t)st;
-  if (bad && st) atomicAdd(bad, 1u);
+  if (bad && (st & ~MI_ST_L4_NONE)) atomicAdd(bad, 1u);
   if (d.cflags) rx_offload_store(d, r, i, off, ih, hdr_ok, l4_ok, ip, l4);
 }
 
@@ -696,17 +781,35 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
     IpHdr ih;
     bool hdr_ok, do_l4;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l);
+    const bool demux = d.flags & MI_BATCH_DEMUX;
+    ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux);
     const bool ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
     if (lane == 0 && ok) {
       const bool odd = ((uintptr_t)d.base + off) & 1u;
-      if (do_l4) {
+      const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
+      if (do_l4 && demux && (ip_off & 0x3fffu)) {
+        // a fragment: ip_fragment summed the datagram before cutting it
+      } else if (do_l4 && (ih.proto == 6u || ih.proto == 17u)) {
         uint32_t sl = fold16(sum_l);
         if (odd) sl = swap16(sl);
         uint32_t c = ~sl & 0xffffu;
         if (ih.proto == 17u && c == 0u) c = 0xffffu;
         const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
         if (at + 2u <= flen) {
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+        }
+      } else if (do_l4) {
+        // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
+        const bool carp = ih.proto == 112u;
+        const uint32_t plen = ih.iplen - ih.hl, span = carp ? 36u : plen;
+        if (plen >= (carp ? 36u : 8u)) {
+          const uint32_t at = ih.hl + (carp ? 6u : 2u);
+          const uint32_t b0 = ld_byte(r, off + at), b1 = ld_byte(r, off + at + 1u);
+          const uint32_t field = odd ? (b0 << 8) + b1 : b0 + (b1 << 8);  // abs lanes, at even
+          uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l) - field);
+          if (odd) sl = swap16(sl);
+          const uint32_t c = ~sl & 0xffffu;
           __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
         }

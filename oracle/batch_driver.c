@@ -60,7 +60,77 @@ struct job {
 	uint32_t fixed_flen, lo, hi;
 	uint16_t *ip_out, *l4_out;
 	uint8_t *status;
+	int demux;
 };
+
+static inline uint32_t be16(const uint8_t *p)
+{
+	return ((uint32_t)p[0] << 8) | p[1];
+}
+
+/*
+ * MI_BATCH_DEMUX: the L4 value the protocol input
+ * routine ip_input hands the datagram to would test, called the way that
+ * routine calls the checksum.  ip_input has trimmed the mbuf to ip_len
+ * (ip_input.c:500-505); the length checks are the routines' own drops.
+ */
+static uint16_t demux_l4(const uint8_t *ip, uint32_t hl, uint32_t iplen, uint8_t *st)
+{
+	union drv_mbuf mb, mp;
+	const uint32_t plen = iplen - hl;
+	uint32_t ulen;
+	memset(&mb, 0, sizeof(mb));
+	mb.m.m_data = (char *)ip;
+	mb.m.m_len = (int32_t)iplen;
+	/* the protocol header's mbuf view: m_data += hlen; m_len -= hlen */
+	memset(&mp, 0, sizeof(mp));
+	mp.m.m_data = (char *)ip + hl;
+	mp.m.m_len = (int32_t)plen;
+	if (be16(ip + 6) & 0x3fff) {	/* IP_MF | IP_OFFMASK: ip_reass (ip_input.c:759-770) */
+		*st |= ORC_ST_L4_NONE;
+		return 0;
+	}
+	switch (ip[9]) {
+	case 6:		/* tcp_input.c:688-693 (pullup fails: tcps_rcvshort), :697-716 */
+		if (plen < 20)
+			break;
+		return F(in_cksum_pseudo_header)(&mb.m, (int)plen, (int)hl,
+		    ld32(ip + 12), ld32(ip + 16), 6);
+	case 17:	/* udp_usrreq.c:375-381 (udps_hdrops), :406-414, :429-451 */
+		if (plen < 8)
+			break;
+		ulen = be16(ip + hl + 4);
+		if (ulen != plen) {
+			if (ulen > plen || ulen < 8)
+				break;	/* udps_badlen */
+			mb.m.m_len = (int32_t)(hl + ulen);	/* m_adj(m, len - ip_len) */
+		}
+		if (be16(ip + hl + 6) == 0) {	/* udps_nosum */
+			*st |= ORC_ST_L4_NONE;
+			return 0;
+		}
+		return F(in_cksum_pseudo_header)(&mb.m, (int)ulen, (int)hl,
+		    ld32(ip + 12), ld32(ip + 16), 17);
+	case 1:		/* ip_icmp.c:336 icmplen = ntohs(ip_len); :374-378 pullup to
+			   hlen + min(icmplen, ICMP_ADVLENMIN) of an ip_len-byte packet */
+		if (iplen < hl + (iplen < 36 ? iplen : 36))
+			break;
+		return F(in_cksum_skip)(&mp.m, (int)iplen, 0);	/* :381-383, truncates */
+	case 2:		/* igmp.c:1445-1452, :1475-1478 */
+		if (plen < 8)
+			break;
+		return F(in_cksum_skip)(&mp.m, (int)plen, 0);
+	case 112:	/* ip_carp.c:600-607 (carps_badlen), :641-643 */
+		if (plen < 36)
+			break;
+		return F(in_cksum_skip)(&mp.m, 36, 0);
+	default:
+		*st |= ORC_ST_L4_NONE;
+		return 0;
+	}
+	*st |= ORC_ST_MALFORMED;
+	return 0;
+}
 
 static void verify_range(const struct job *j)
 {
@@ -85,6 +155,8 @@ static void verify_range(const struct job *j)
 				                   : F(in_cksum_skip)(&mb.m, (int)hl, 0);
 				if (iplen < hl || iplen > fl)
 					st |= ORC_ST_MALFORMED;
+				else if (j->demux)
+					l4 = demux_l4(ip, hl, iplen, &st);
 				else
 					l4 = F(in_cksum_pseudo_header)(&mb.m, (int)(iplen - hl),
 					    (int)hl, ld32(ip + 12), ld32(ip + 16), ip[9]);
@@ -119,7 +191,26 @@ static void finalize_range(const struct job *j)
 		memset(&mb, 0, sizeof(mb));
 		mb.m.m_data = (char *)ip;
 		mb.m.m_len = (int32_t)fl;
-		if (ip[9] == 6 || ip[9] == 17) {
+		if (j->demux && (be16(ip + 6) & 0x3fff)) {
+			/* a fragment: ip_fragment sums the whole datagram
+			   before cutting it (ip_output.c:930,950) */
+		} else if (j->demux && (ip[9] == 1 || ip[9] == 2 || ip[9] == 112)) {
+			/* icmp_send ip_icmp.c:889-891, igmp.c:2184-2185 / :3483,
+			   carp_send_ad ip_carp.c:944,985: field = 0, in_cksum
+			   over the message from the header on */
+			const uint32_t plen = iplen - hl, carp = ip[9] == 112;
+			if (plen >= (carp ? 36u : 8u)) {
+				union drv_mbuf mp;
+				uint8_t *f = ip + hl + (carp ? 6 : 2);
+				uint16_t c;
+				memset(&mp, 0, sizeof(mp));
+				mp.m.m_data = (char *)ip + hl;
+				mp.m.m_len = (int32_t)plen;
+				f[0] = f[1] = 0;
+				c = F(in_cksum_skip)(&mp.m, carp ? 36 : (int)plen, 0);
+				memcpy(f, &c, 2);
+			}
+		} else if (ip[9] == 6 || ip[9] == 17) {
 			uint16_t c = F(in_cksum_skip)(&mb.m, (int)iplen, (int)hl);
 			uint32_t at = hl + (ip[9] == 6 ? 16u : 6u);
 			if (ip[9] == 17 && c == 0)
@@ -177,7 +268,7 @@ void F(ipv4_verify_batch)(const uint8_t *base, const uint64_t *offs,
     uint8_t *status, int nthreads)
 {
 	struct job j = { base, NULL, offs, stride, first_off, flen, fixed_flen,
-	                 0, n, ip_out, l4_out, status };
+	                 0, n, ip_out, l4_out, status, 0 };
 	run_jobs(&j, n, nthreads, verify_thr);
 }
 
@@ -186,7 +277,26 @@ void F(ipv4_finalize_batch)(uint8_t *base, const uint64_t *offs,
     uint32_t fixed_flen, uint32_t n, int nthreads)
 {
 	struct job j = { base, base, offs, stride, first_off, flen, fixed_flen,
-	                 0, n, NULL, NULL, NULL };
+	                 0, n, NULL, NULL, NULL, 0 };
+	run_jobs(&j, n, nthreads, finalize_thr);
+}
+
+void F(ipv4_demux_verify_batch)(const uint8_t *base, const uint64_t *offs,
+    uint64_t stride, uint64_t first_off, const uint32_t *flen,
+    uint32_t fixed_flen, uint32_t n, uint16_t *ip_out, uint16_t *l4_out,
+    uint8_t *status, int nthreads)
+{
+	struct job j = { base, NULL, offs, stride, first_off, flen, fixed_flen,
+	                 0, n, ip_out, l4_out, status, 1 };
+	run_jobs(&j, n, nthreads, verify_thr);
+}
+
+void F(ipv4_demux_finalize_batch)(uint8_t *base, const uint64_t *offs,
+    uint64_t stride, uint64_t first_off, const uint32_t *flen,
+    uint32_t fixed_flen, uint32_t n, int nthreads)
+{
+	struct job j = { base, base, offs, stride, first_off, flen, fixed_flen,
+	                 0, n, NULL, NULL, NULL, 1 };
 	run_jobs(&j, n, nthreads, finalize_thr);
 }
 

@@ -76,6 +76,7 @@ uint16_t orc_in_addword(uint16_t a, uint16_t b);
 #define ORC_ST_IP_BAD    1u
 #define ORC_ST_L4_BAD    2u
 #define ORC_ST_MALFORMED 4u
+#define ORC_ST_L4_NONE   8u	/* demux: no L4 checksum applies */
 
 /*
  * tx_copy_batch (TX checksum offload fused with the driver's copy,
@@ -98,6 +99,13 @@ uint16_t orc_in_addword(uint16_t a, uint16_t b);
 	    uint32_t fixed_flen, uint32_t n, uint16_t *ip_out, uint16_t *l4_out,    \
 	    uint8_t *status, int nthreads);                                         \
 	void PFX##ipv4_finalize_batch(uint8_t *base, const uint64_t *offs,         \
+	    uint64_t stride, uint64_t first_off, const uint32_t *flen,              \
+	    uint32_t fixed_flen, uint32_t n, int nthreads);                         \
+	void PFX##ipv4_demux_verify_batch(const uint8_t *base,                      \
+	    const uint64_t *offs, uint64_t stride, uint64_t first_off,              \
+	    const uint32_t *flen, uint32_t fixed_flen, uint32_t n,                  \
+	    uint16_t *ip_out, uint16_t *l4_out, uint8_t *status, int nthreads);     \
+	void PFX##ipv4_demux_finalize_batch(uint8_t *base, const uint64_t *offs,   \
 	    uint64_t stride, uint64_t first_off, const uint32_t *flen,              \
 	    uint32_t fixed_flen, uint32_t n, int nthreads);                         \
 	uint64_t PFX##skip_repeat(const uint8_t *buf, int len, int iters);          \

@@ -89,6 +89,10 @@ class Oracle:
         self._final = g("ipv4_finalize_batch"); self._final.restype = None
         self._final.argtypes = [C.c_void_p, u64p, C.c_uint64, C.c_uint64, u32p, C.c_uint32,
                                 C.c_uint32, C.c_int]
+        self._dverify = g("ipv4_demux_verify_batch"); self._dverify.restype = None
+        self._dverify.argtypes = self._verify.argtypes
+        self._dfinal = g("ipv4_demux_finalize_batch"); self._dfinal.restype = None
+        self._dfinal.argtypes = self._final.argtypes
         self._repeat = g("skip_repeat"); self._repeat.restype = C.c_uint64
         self._repeat.argtypes = [C.c_void_p, C.c_int, C.c_int]
         self._tx = g("tx_copy_batch"); self._tx.restype = None
@@ -134,19 +138,23 @@ class Oracle:
 
     # --- batch drivers ------------------------------------------------------
     def ipv4_verify_batch(self, buf: np.ndarray, n: int, *, offs=None, stride: int = 0,
-                          first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1):
+                          first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1,
+                          demux: bool = False):
+        """RX verify; ``demux`` = the MI_BATCH_DEMUX protocol dispatch
+        (batch_driver.c demux_l4)."""
         ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
         offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
         flen = None if flen is None else np.ascontiguousarray(flen, np.uint32)
-        self._verify(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
+        (self._dverify if demux else self._verify)(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
                      fixed_flen, n, _ptr(ip, u16p), _ptr(l4, u16p), _ptr(st, u8p), nthreads)
         return ip, l4, st
 
     def ipv4_finalize_batch(self, buf: np.ndarray, n: int, *, offs=None, stride: int = 0,
-                            first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1):
+                            first_off: int = 0, flen=None, fixed_flen: int = 0, nthreads: int = 1,
+                            demux: bool = False):
         offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
         flen = None if flen is None else np.ascontiguousarray(flen, np.uint32)
-        self._final(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
+        (self._dfinal if demux else self._final)(buf.ctypes.data, _ptr(offs, u64p), stride, first_off, _ptr(flen, u32p),
                     fixed_flen, n, nthreads)
 
     def skip_repeat(self, buf: np.ndarray, length: int, iters: int) -> int:

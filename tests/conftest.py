@@ -9,6 +9,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "cksum_golden.npz")
+DEMUX_GOLDEN = os.path.join(ROOT, "tests", "golden", "demux_golden.npz")
 
 
 def pytest_configure(config):
@@ -32,6 +33,12 @@ def pytest_collection_modifyitems(config, items):
 @pytest.fixture(scope="session")
 def golden():
     with np.load(GOLDEN, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def demux_golden():
+    with np.load(DEMUX_GOLDEN, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
 
 

@@ -154,3 +154,64 @@ def test_port_matches_reference_random():
             a, b = int(rng.integers(2**32)), int(rng.integers(2**32))
             p = int(rng.integers(256))
             assert PORT.chain_pseudo(segs, plen, 20, a, b, p) == ref.chain_pseudo(segs, plen, 20, a, b, p)
+
+
+# ------------------------------- MI_BATCH_DEMUX (small-header callers) golden
+def test_golden_demux(demux_golden):
+    """tests/golden/demux_golden.npz came from the reference's in_cksum.c
+    driven as ip_input's protocol input routines call it; the restatement
+    reproduces every datagram (finalize bytes, verify ip / l4 / status)."""
+    g = demux_golden
+    n = len(g["offs"])
+    _, fin = aligned(g["fin_in"])
+    PORT.ipv4_finalize_batch(fin, n, offs=g["offs"], flen=g["flen"], demux=True)
+    assert np.array_equal(fin, g["fin_out"])
+    _, ver = aligned(g["ver_in"])
+    ip, l4, st = PORT.ipv4_verify_batch(ver, n, offs=g["offs"], flen=g["flen"], demux=True, nthreads=3)
+    assert np.array_equal(ip, g["ip"]) and np.array_equal(l4, g["l4"]) and np.array_equal(st, g["st"])
+
+
+def test_demux_rules_statement(demux_golden):
+    """A second, Python statement of the demux length / protocol rules
+    (include/mi_cksum.h) agrees with the golden status bits and with the
+    contract sum over each protocol's span."""
+    g = demux_golden
+    buf, offs, flen = g["ver_in"], g["offs"], g["flen"]
+    for i in range(len(offs)):
+        p, fl = int(offs[i]), int(flen[i])
+        st = int(g["st"][i])
+        if fl < 20 or (buf[p] & 15) * 4 < 20 or (buf[p] & 15) * 4 > fl:
+            assert st == 4
+            continue
+        hl = (int(buf[p]) & 15) * 4
+        iplen = (int(buf[p + 2]) << 8) | int(buf[p + 3])
+        if iplen < hl or iplen > fl:
+            assert st & 4 and int(g["l4"][i]) == 0
+            continue
+        plen, proto = iplen - hl, int(buf[p + 9])
+        a = [int(x) for x in buf[p + 12:p + 20]]
+        addr = a[0] + a[2] + a[4] + a[6] + ((a[1] + a[3] + a[5] + a[7]) << 8)
+        frag = ((int(buf[p + 6]) << 8) | int(buf[p + 7])) & 0x3FFF
+        d = bytes(buf[p + hl:p + iplen])
+        want_l4, want_st = 0, 0
+        if frag or proto not in (6, 17, 1, 2, 112):
+            want_st = 8
+        elif plen < {6: 20, 17: 8, 1: 36, 2: 8, 112: 36}[proto]:
+            want_st = 4
+        elif proto == 17:
+            ulen = (d[4] << 8) | d[5]
+            if ulen != plen and (ulen > plen or ulen < 8):
+                want_st = 4
+            elif (d[6] << 8 | d[7]) == 0:
+                want_st = 8
+            else:
+                seed = addr + (17 << 8) + (((ulen & 0xFF) << 8) | (ulen >> 8))
+                want_l4 = contract_stream(d[:ulen], seed)
+        elif proto == 6:
+            seed = addr + (6 << 8) + (((plen & 0xFF) << 8) | (plen >> 8))
+            want_l4 = contract_stream(d, seed)
+        else:
+            want_l4 = contract_stream(d[:36] if proto == 112 else d)
+        assert int(g["l4"][i]) == want_l4, i
+        ip_bad = 1 if int(g["ip"][i]) else 0
+        assert st == want_st | ip_bad | (2 if want_l4 else 0), i

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 OUT=gpurun_out
 BENCH_ARGS=${BENCH_ARGS:-}
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 300 python bench.py $BENCH_ARGS > $OUT/bench.json 2> $OUT/bench.err && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/prof -o run --output-format csv -- \
