@@ -122,6 +122,9 @@ typedef struct mi_pkt_batch {
  * plain in_cksum, fragments and other protocols none.  See
  * mi_cksum_ipv4_verify and mi_cksum_ipv4_finalize. */
 #define MI_BATCH_DEMUX  2u
+/* MI_BATCH_HOST_STAGED: mi_cksum_ipv4_verify_host copies through device
+ * staging even when the batch is registered (mapped) host memory. */
+#define MI_BATCH_HOST_STAGED 4u
 
 /* Lane conventions for mi_cksum_span_batch. */
 #define MI_SPAN_STREAM 0u  /* in_cksum_skip / in_cksum_pseudo_header: lanes
@@ -345,15 +348,21 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream);
 
 /*
  * Host-resident batch (the path's real start and end: DPDK mbufs in host
- * memory).  b->base / offs / lens are HOST pointers (page-locked memory gives
- * full PCIe rate).  The batch is cut into chunks that are copied to device
- * staging and verified on a ring of streams (H2D || kernel || D2H); outputs
- * are host arrays.  Synchronous: returns when outputs are written.
+ * memory).  b->base / offs / lens are HOST pointers; outputs are host arrays.
+ * Synchronous: returns when outputs are written.  Two ways across PCIe:
+ *   zero-copy -- base 16-byte aligned and [base, base + roundup16(bytes))
+ *     inside a range registered with mi_cksum_host_register: the verify
+ *     kernel reads the datagrams in place over the link (no staging copy, no
+ *     DMA engine, slot gaps never cross); descriptors go H2D once;
+ *   staged -- otherwise, or with MI_BATCH_HOST_STAGED: the batch is cut into
+ *     chunks copied to device staging and verified on a ring of streams
+ *     (H2D || kernel || D2H; fixed slots copied pitched, envelopes only).
  */
 int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                               uint8_t *status, uint32_t *bad_count);
 
-/* Page-lock / unlock a host range for mi_cksum_ipv4_verify_host (hipHostRegister). */
+/* Page-lock and map / unlock a host range for mi_cksum_ipv4_verify_host
+ * (hipHostRegister, mapped + portable). */
 int mi_cksum_host_register(void *p, uint64_t bytes);
 int mi_cksum_host_unregister(void *p);
 

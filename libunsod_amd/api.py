@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_DEMUX, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -343,15 +343,17 @@ def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
 
 
 def ipv4_verify_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
-                     fixed_len: int = 0):
-    """Host-resident batch: chunked H2D -> verify -> D2H.  Returns numpy
-    (ip, l4, status, bad_count).  Page-lock ``buf`` (host_register) for full
-    PCIe rate."""
+                     fixed_len: int = 0, staged: bool = False, demux: bool = False):
+    """Host-resident batch (mi_cksum_ipv4_verify_host).  Returns numpy
+    (ip, l4, status, bad_count).  A ``buf`` registered with host_register is
+    read in place by the kernel over PCIe (zero-copy) unless ``staged``;
+    otherwise chunked H2D -> verify -> D2H."""
     offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
     lens = None if lens is None else np.ascontiguousarray(lens, np.uint32)
     hb = PktBatchC(buf.ctypes.data, buf.nbytes, None if offs is None else offs.ctypes.data, stride, first_off,
                    None if lens is None else lens.ctypes.data, fixed_len, n,
-                   int(lens.max()) if lens is not None and n else fixed_len, 0)
+                   int(lens.max()) if lens is not None and n else fixed_len,
+                   (MI_BATCH_HOST_STAGED if staged else 0) | (MI_BATCH_DEMUX if demux else 0))
     ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
     bad = C.c_uint32(0)
     check("mi_cksum_ipv4_verify_host",

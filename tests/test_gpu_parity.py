@@ -234,6 +234,41 @@ def test_host_path_matches_device():
     assert bad == 0 and not st.any()
 
 
+@pytest.mark.parametrize("layout", ["slots", "packed"])
+def test_host_zero_copy(layout):
+    """Registered host batches are read in place over PCIe (zero-copy) and
+    give the same results as the staged copy path and the oracle; an
+    unregistered sub-range falls back to staging."""
+    if layout == "slots":
+        n, L, stride, first = 3000, 1500, 2176, 142
+        b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=15)
+        lay = dict(stride=stride, first_off=first, fixed_len=L)
+        olay = dict(stride=stride, first_off=first, fixed_flen=L)
+        fin = dict(stride=stride, first_off=first, fixed_flen=L)
+    else:
+        n = 4000
+        lens = synth.pareto_lengths(n, seed=19)
+        offs = synth.packed_offsets(lens, first_off=6)
+        b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=16)
+        lay = dict(offs=offs, lens=lens)
+        olay = fin = dict(offs=offs, flen=lens.astype(np.uint32))
+    keep, host = aligned(b0["buf"], 4096)
+    ORC.ipv4_finalize_batch(host, n, **fin)
+    rng = np.random.default_rng(3)
+    host[rng.choice(host.size, 25, replace=False)] ^= 0x40
+    want = ORC.ipv4_verify_batch(host, n, **olay)
+    mi.host_register(host)
+    try:
+        for staged in (False, True):
+            ip, l4, st, bad = mi.ipv4_verify_host(host, n, staged=staged, **lay)
+            assert np.array_equal(ip, want[0]) and np.array_equal(l4, want[1]), staged
+            assert np.array_equal(st, want[2]) and bad == int((want[2] != 0).sum()), staged
+    finally:
+        mi.host_unregister(host)
+    ip, l4, st, bad = mi.ipv4_verify_host(host, n, **lay)  # no longer registered: staged
+    assert np.array_equal(st, want[2])
+
+
 def test_deterministic_and_stream_async():
     n, L = 8192, 1500
     buf = torch.empty(142 + n * 2176 + 64, dtype=torch.uint8, device="cuda")
