@@ -1224,8 +1224,22 @@ __device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, cons
   return v;
 }
 
+// Fast path of k_tx_copy: chunk-major gather with unaligned loads.  Every
+// nonempty mbuf of the frame (at most kTxSeg of them: the header mbuf and the
+// payload's cluster pieces) is kept as (frame position, source - position) in
+// registers; destination chunk ci (frame bytes [q0, q0 + 16), q0 = 16 ci - h)
+// takes each overlapping segment's bytes with ONE 16-byte load at the
+// segment's source address of q0 (gfx950 buffer loads accept any byte
+// address, tools/unaligned_probe.hip) -- no funnel shifts, no neighbour-lane
+// exchange -- and all of a pass's loads are issued before any is used.  A
+// load that would start before the source buffer or run past its end takes a
+// per-byte path instead (the first / last bytes of the buffer only).
+constexpr int kTxSeg = 4;
+
 template <int G, int U>
-__global__ __launch_bounds__(kBlock, TX_WAVES) void k_tx_copy(TxDesc t) {
+__global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
+  static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
+  __shared__ uint32_t s_seg[kBlock / G][kTxSeg][2];
   Desc ds{}, dd{};
   ds.base = t.src;
   ds.bytes = t.src_bytes;
@@ -1233,38 +1247,42 @@ __global__ __launch_bounds__(kBlock, TX_WAVES) void k_tx_copy(TxDesc t) {
   dd.bytes = t.dst_bytes;
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
   const int lane = threadIdx.x & (G - 1);
+  const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
   for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < t.n; i += stride) {
     const uint32_t len = t.pkt_len[i];
     const uint32_t k0 = t.pkt_seg[i], k1 = t.pkt_seg[i + 1];
-    const uint32_t nseg = k1 - k0;
     const uint32_t l3 = t.l3;
     const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
     const uint32_t h = D & 15u, c0 = D & ~15u;
     uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
     // walk 1: bytes in the chain, the IP mbuf (segment holding frame byte l3)
-    // and its m_len from the IP header on
-    uint32_t total = 0, ip_mlen = 0, kip = 0;
+    // and its m_len from the IP header on, and the first kTxSeg nonempty
+    // segments (frame start, source offset - frame start) into LDS
+    uint32_t total = 0, ip_mlen = 0, m = 0;
     for (uint32_t w = k0; w < k1 && !st; w += G) {
       const uint32_t k = w + lane;
       const uint32_t l = k < k1 ? (uint32_t)max(t.seg_len[k], 0) : 0u;
       const uint32_t inc = group_scan<G>(l);
       const uint32_t a = total + inc - l, e = total + inc;
+      const uint32_t nz = l ? 1u : 0u;
+      const uint32_t zi = group_scan<G>(nz);
+      const uint32_t idx = m + zi - nz;
+      if (nz && idx < (uint32_t)kTxSeg) {
+        s_seg[grp][idx][0] = a;
+        s_seg[grp][idx][1] = (uint32_t)t.seg_off[k] - a;
+      }
       const bool isip = l && a <= l3 && l3 < e;
       ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
-      kip += group_sum<G>(isip ? k - k0 : 0u);
       total += group_lane<G>(inc, G - 1);
+      m += group_lane<G>(zi, G - 1);
     }
     if (!st && total < len) st = MI_TX_SHORT;
-#ifdef TX_DEBUG
-    if (i < 2) printf("i=%u lane=%d len=%u k0=%u k1=%u total=%u ip_mlen=%u kip=%u st=%u seglen=%d\n", i, lane, len, k0, k1, total, ip_mlen, kip, st, (int)(k0 + lane < k1 ? t.seg_len[k0 + lane] : -1));
-#endif
     if (st) {
       if (lane == 0) t.status[i] = (uint8_t)st;
       continue;
     }
     ip_mlen = group_lane<G>(ip_mlen, 0);
-    kip = group_lane<G>(kip, 0);
     const bool odd = (h + l3) & 1u;  // parity of the IP header's destination address
     IpHdr ih{};
     bool ok = false, do_ip = false, do_l4 = false, udp = false, done = false;
@@ -1302,74 +1320,117 @@ __global__ __launch_bounds__(kBlock, TX_WAVES) void k_tx_copy(TxDesc t) {
         if (ci < clast) store_chunk(rd, c0 + 16u * ci, v[u], pa - cs, pe - cs);
       }
     };
-    if (nseg <= (uint32_t)G && ip_mlen >= 20u) {
-      // ---- fast path: segment-major.  The IP mbuf's first chunks stay in
-      // registers (header parse, sum-field patches); every other chunk is
-      // gathered, folded and stored as it streams by.
-      const uint32_t k = k0 + lane;
-      const bool hs = (uint32_t)lane < nseg;
-      const int sl = hs ? max(t.seg_len[k], 0) : 0;
-      const uint32_t so = hs ? (uint32_t)t.seg_off[k] : 0u;
-      const int sa = (int)group_scan<G>((uint32_t)sl) - sl;
-      auto piece = [&](uint32_t j) {
-        Piece pc;
-        pc.pa = (int)group_lane<G>((uint32_t)sa, j);
-        pc.pe = min(pc.pa + (int)group_lane<G>((uint32_t)sl, j), (int)len);
-        pc.del = group_lane<G>(so, j) - (uint32_t)pc.pa;
-        pc.cfirst = (h + pc.pa) >> 4;
-        pc.clast = pc.pe > pc.pa ? (h + pc.pe + 15u) >> 4 : pc.cfirst;
-        return pc;
-      };
-      // stream pass p of piece pc: gather, fold, store (u >= u0)
-      auto stream = [&](const Piece &pc, uint32_t p, const u32x4 (&x)[U + 1], int u0) {
+    if (m <= (uint32_t)kTxSeg) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // segment e covers frame bytes [S[e], S[e+1]) (the last one: to len),
+      // frame byte q sits at source offset q + Dl[e]
+      int S[kTxSeg + 2];
+      uint32_t Dl[kTxSeg];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < u0) continue;
-          const u32x4 v = make_chunk<G, U>(x, u, pc, p, lane, h);
-          const uint32_t ci = pc.cfirst + p * (G * U) + u * G + lane;
-          const int cs = (int)(16u * ci) - (int)h;
-          fold_chunk(v, cs - (int)l3, lend, hend, hend > 20, acc_t, acc_h, acc_f);
-          if (ci < pc.clast) store_chunk(rd, c0 + 16u * ci, v, pc.pa - cs, pc.pe - cs);
-        }
-      };
-      const Piece ipc = piece(kip);
-      u32x4 held;
-      {
-        u32x4 x[U + 1];
-        load_pass<G, U>(rs, ipc, 0, lane, h, x);
-        u32x4 hv[1] = {make_chunk<G, U>(x, 0, ipc, 0, lane, h)};
-        decide1(hv[0], h + l3 - 16u * ipc.cfirst);
-        held = hv[0];
-        const uint32_t pip = l3 + 10u, pl4 = l3 + at;
-        const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-        const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
-        done = (uint64_t)need + h <= 16ull * (ipc.cfirst + G);  // the patches land in held
-        if (done) {
-          fold_chunk(held, (int)(16u * (ipc.cfirst + lane)) - (int)(h + l3), lend, hend, hend > 20, acc_t,
-                     acc_h, acc_f);
-          stream(ipc, 0, x, 1);
-        }
+      for (int e = 0; e < kTxSeg; ++e) {
+        S[e] = (uint32_t)e < m ? (int)s_seg[grp][e][0] : (int)len;
+        Dl[e] = (uint32_t)e < m ? s_seg[grp][e][1] : 0u;
       }
-      if (done) {
-        for (uint32_t p = 1; p * (G * U) < ipc.clast - ipc.cfirst; ++p) {
-          u32x4 x[U + 1];
-          load_pass<G, U>(rs, ipc, p, lane, h, x);
-          stream(ipc, p, x, 0);
-        }
-        for (uint32_t j = 0; j < nseg; ++j) {
-          if (j == kip) continue;
-          const Piece pc = piece(j);
-          for (uint32_t p = 0; p * (G * U) < pc.clast - pc.cfirst; ++p) {
-            u32x4 x[U + 1];
-            load_pass<G, U>(rs, pc, p, lane, h, x);
-            stream(pc, p, x, 0);
+      S[kTxSeg] = S[kTxSeg + 1] = (int)len;
+#pragma unroll
+      for (int e = 0; e < kTxSeg; ++e) S[e] = min(S[e], (int)len);
+      const uint32_t nch = (h + len + 15u) >> 4;
+      const uint32_t npass = (nch + G * U - 1) / (G * U);
+      // Chunk ci of the frame, gathered.  Its bytes [max(q0, 0), min(q0 + 16,
+      // len)) come from segment j (the one holding the first byte) and, when
+      // the chunk crosses a segment end, j + 1: two loads at most, issued by
+      // `issue`, merged by `build`.  A chunk touching three segments (an mbuf
+      // shorter than 16 bytes) or a load crossing the source buffer's ends is
+      // assembled byte by byte (rare).
+      struct Cut {
+        int q0, lo, mid, hi;  // frame bytes [lo, mid) from j, [mid, hi) from j + 1
+        int64_t A1, A2;
+        bool slow;
+      };
+      auto cut = [&](uint32_t ci) {
+        Cut c;
+        c.q0 = (int)(16u * ci) - (int)h;
+        c.lo = max(c.q0, 0);
+        c.hi = min(c.q0 + 16, (int)len);
+        uint32_t j = 0;
+#pragma unroll
+        for (int e = 1; e < kTxSeg; ++e) j += c.lo >= S[e] ? 1u : 0u;
+        int s1 = (int)len, s2 = (int)len;
+        uint32_t d0 = Dl[0], d1 = 0;
+#pragma unroll
+        for (int e = 0; e < kTxSeg; ++e) {
+          if ((uint32_t)e == j) {
+            d0 = Dl[e];
+            s1 = S[e + 1];
+            if (e + 1 < kTxSeg) {
+              d1 = Dl[e + 1];
+              s2 = S[e + 2];
+            }
           }
         }
+        c.mid = min(s1, c.hi);
+        c.A1 = (int64_t)c.q0 + (int64_t)(int32_t)d0;
+        c.A2 = (int64_t)c.q0 + (int64_t)(int32_t)d1;
+        const bool two = c.mid < c.hi;
+        c.slow = c.lo < c.hi &&
+                 ((two && s2 < c.hi) || c.A1 < 0 || c.A1 + 16 > (int64_t)t.src_bytes ||
+                  (two && (c.A2 < 0 || c.A2 + 16 > (int64_t)t.src_bytes)));
+        return c;
+      };
+      auto issue = [&](uint32_t ci, u32x4 (&x)[2]) {
+        const Cut c = cut(ci);
+        const bool ok1 = c.lo < c.hi && !c.slow, ok2 = ok1 && c.mid < c.hi;
+        x[0] = ld16(rs, ok1 ? (uint32_t)c.A1 : kOOB);
+        x[1] = ld16(rs, ok2 ? (uint32_t)c.A2 : kOOB);
+      };
+      auto build = [&](uint32_t ci, const u32x4 (&x)[2]) {
+        const Cut c = cut(ci);
+        u32x4 v{0, 0, 0, 0};
+        if (!c.slow) {
+          merge_bytes(v, x[0], c.lo - c.q0, c.mid - c.q0);
+          merge_bytes(v, x[1], c.mid - c.q0, c.hi - c.q0);
+        } else {
+          for (int q = c.lo; q < c.hi; ++q) {
+            uint32_t d = Dl[0];
+#pragma unroll
+            for (int e = 1; e < kTxSeg; ++e) d = q >= S[e] ? Dl[e] : d;
+            put_byte(v, q - c.q0, ld_byte(rs, (uint32_t)(q + (int)d)));
+          }
+        }
+        return v;
+      };
+      u32x4 held{0, 0, 0, 0};
+      for (uint32_t p = 0; p < npass; ++p) {
+        u32x4 x[U][2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) issue(p * (G * U) + u * G + lane, x[u]);
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = build(p * (G * U) + u * G + lane, x[u]);
+        if (p == 0) {
+          decide1(v[0], h + l3);
+          const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+          const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+          const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
+          if ((uint64_t)need + h > 16ull * G) break;  // a sum field beyond the held chunks: generic path
+          done = true;
+          held = v[0];
+        }
+        fold_all(v, 0, p);
+        store_all(v, 0, nch, p, 0, (int)len, p == 0 ? 1 : 0);
+      }
+      if (npass == 0) {
+        ok = do_ip = do_l4 = false;
+        done = true;
+      }
+      if (done) {
         const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
         uint32_t c_ip, c_l4;
         tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
         const uint32_t pip = l3 + 10u, pl4 = l3 + at;
-        const int b0 = (int)h - (int)(16u * (ipc.cfirst + lane));  // frame offset -> byte of held
+        const int b0 = (int)h - (int)(16u * lane);  // frame position -> byte of held
         if (do_ip) {
           if (pip < len) put_byte(held, (int)pip + b0, c_ip);
           if (pip + 1u < len) put_byte(held, (int)pip + 1 + b0, c_ip >> 8);
@@ -1378,12 +1439,13 @@ __global__ __launch_bounds__(kBlock, TX_WAVES) void k_tx_copy(TxDesc t) {
           if (pl4 < len) put_byte(held, (int)pl4 + b0, c_l4);
           if (pl4 + 1u < len) put_byte(held, (int)pl4 + 1 + b0, c_l4 >> 8);
         }
-        const uint32_t ci = ipc.cfirst + lane;
+        const uint32_t ci = lane;
         const int cs = (int)(16u * ci) - (int)h;
-        if (ci < ipc.clast) store_chunk(rd, c0 + 16u * ci, held, ipc.pa - cs, ipc.pe - cs);
+        if (ci < nch) store_chunk(rd, c0 + 16u * ci, held, -cs, (int)len - cs);
         if (lane == 0)
           t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
       }
+      __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
     }
 #ifndef TX_NO_GENERIC
     if (!done) {
@@ -1747,7 +1809,7 @@ int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
 // TX copy shapes: G = 8 or 16 (row-local DPP neighbour exchange; the IP
 // header sits in the u = 0 chunks of lanes 0..G-1).  Long pieces loop over
 // passes of G*U chunks.
-#define FOR_TX_GU(X) X(8, 2) X(8, 4) X(8, 8) X(16, 2) X(16, 4) X(16, 6) X(16, 8)
+#define FOR_TX_GU(X) X(8, 2) X(8, 4) X(8, 8) X(16, 2) X(16, 4) X(16, 6) X(16, 8) X(32, 2) X(32, 4) X(64, 2) X(64, 4)
 
 Shape pick_tx_shape(uint32_t max_len) {
   static const Shape forced = [] {
@@ -1763,9 +1825,10 @@ Shape pick_tx_shape(uint32_t max_len) {
 #define X(G_, U_) if (g_tune.g == G_ && g_tune.u == U_) return {G_, U_};
   FOR_TX_GU(X)
 #undef X
-  const uint32_t ch = (max_len + 15u + 15u) / 16u;
-  if (ch <= 32) return {8, 4};
-  return {16, 6};
+  // the gather is latency-bound per frame: narrow groups (more frames in
+  // flight per wave) and short passes (occupancy) win -- profiles/tx_sweep_r01.jsonl
+  (void)max_len;
+  return {8, 2};
 }
 
 int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {

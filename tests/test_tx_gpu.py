@@ -38,7 +38,7 @@ def test_tx_copy_matches_oracle(name):
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]} (frame {(bad[0] - c['dst_first']) // c['stride']})"
 
 
-@pytest.mark.parametrize("shape", [(8, 2), (8, 4), (8, 8), (16, 2), (16, 4), (16, 6), (16, 8)])
+@pytest.mark.parametrize("shape", [(8, 2), (8, 4), (8, 8), (16, 2), (16, 4), (16, 6), (16, 8), (32, 2), (32, 4), (64, 2), (64, 4)])
 def test_tx_every_shape(shape):
     try:
         mi.set_shape(*shape)
