@@ -70,9 +70,15 @@ __device__ __forceinline__ uint32_t swap16(uint32_t x) {
   return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu);
 }
 // A dword's two 16-bit lanes, added: the absolute-address lanes of in_cksumdata.
-__device__ __forceinline__ uint32_t halves(uint32_t w) { return (w & 0xffffu) + (w >> 16); }
+// v_dot2_u32_u16 with (1, 1): lo16 + hi16 + acc in one VALU op.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t halves_acc(uint32_t w, uint32_t acc) {
+  const u16x2 one = {1, 1};
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), one, acc, false);
+}
+__device__ __forceinline__ uint32_t halves(uint32_t w) { return halves_acc(w, 0u); }
 __device__ __forceinline__ uint32_t sum4(const u32x4 &v) {
-  return halves(v.x) + halves(v.y) + halves(v.z) + halves(v.w);
+  return halves_acc(v.w, halves_acc(v.z, halves_acc(v.y, halves(v.x))));
 }
 // Bytes [a, b) of dword w, 0 <= a, b <= 4 (64-bit shifts: a shift by 32 is legal).
 __device__ __forceinline__ uint32_t keep(uint32_t w, int a, int b) {
@@ -1063,15 +1069,16 @@ __device__ __forceinline__ Raw2 ld_pair(__amdgpu_buffer_rsrc_t r, uint32_t a) {
   return {ld16(r, A), ld16(r, (a & 15u) ? A + 16u : kOOB)};
 }
 __device__ __forceinline__ u32x4 shift2(const u32x4 &x, const u32x4 &y, uint32_t a) {
+  // named registers and selects only: an array here gets a select-of-index
+  // turned into a dynamic (scratch) access by the optimiser
   const uint32_t s = a & 15u, b = s & 3u;
-  const uint32_t w[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-  uint32_t t[6], z[5];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) t[k] = (s & 8u) ? w[k + 2] : w[k];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) z[k] = (s & 4u) ? t[k + 1] : t[k];
-  return {__builtin_amdgcn_alignbyte(z[1], z[0], b), __builtin_amdgcn_alignbyte(z[2], z[1], b),
-          __builtin_amdgcn_alignbyte(z[3], z[2], b), __builtin_amdgcn_alignbyte(z[4], z[3], b)};
+  const bool h8 = s & 8u, h4 = s & 4u;
+  const uint32_t t0 = h8 ? x.z : x.x, t1 = h8 ? x.w : x.y, t2 = h8 ? y.x : x.z;
+  const uint32_t t3 = h8 ? y.y : x.w, t4 = h8 ? y.z : y.x, t5 = h8 ? y.w : y.y;
+  const uint32_t z0 = h4 ? t1 : t0, z1 = h4 ? t2 : t1, z2 = h4 ? t3 : t2;
+  const uint32_t z3 = h4 ? t4 : t3, z4 = h4 ? t5 : t4;
+  return {__builtin_amdgcn_alignbyte(z1, z0, b), __builtin_amdgcn_alignbyte(z2, z1, b),
+          __builtin_amdgcn_alignbyte(z3, z2, b), __builtin_amdgcn_alignbyte(z4, z3, b)};
 }
 __device__ __forceinline__ u32x4 shift_pair(const Raw2 &p, uint32_t a) { return shift2(p.x, p.y, a); }
 // Bytes [a, b) of a dword as a mask, 0 <= a, b <= 4 (32-bit shifts only).
@@ -1236,6 +1243,68 @@ __device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, cons
 // per-byte path instead (the first / last bytes of the buffer only).
 constexpr int kTxSeg = 4;
 
+// A frame's first kTxSeg nonempty segments: segment e covers frame bytes
+// [S_e, S_e+1) (S_0 = 0, the last one to L), frame byte q of segment e sits
+// at source offset q + D_e.  A 16-byte load at source offset A (u32; a
+// negative offset wraps past lim) is inside the source buffer iff A <= lim.
+struct TxSegs {
+  int S1, S2, S3, L;
+  uint32_t D0, D1, D2, D3, lim;
+};
+// Destination chunk ci (frame bytes [q0, q0 + 16), q0 = 16 ci - h): bytes
+// [max(q0, 0), q0 + B) come from segment j (the one holding the first byte,
+// loaded at A1), [q0 + B, min(q0 + 16, L)) from segment j + 1 (at A2) when
+// `two`.  clip: the chunk is cut by the frame's ends.  slow: it touches three
+// segments or a load would leave the source buffer.
+struct TxCut {
+  int q0, B;
+  uint32_t A1, A2;
+  bool two, clip, slow;
+};
+__device__ __forceinline__ TxCut tx_cut(const TxSegs &g, uint32_t ci, uint32_t h) {
+  TxCut c;
+  c.q0 = (int)(16u * ci) - (int)h;
+  const int q = max(c.q0, 0), hi = min(c.q0 + 16, g.L);
+  const bool j1 = q >= g.S1, j2 = q >= g.S2, j3 = q >= g.S3;
+  const uint32_t d0 = j3 ? g.D3 : j2 ? g.D2 : j1 ? g.D1 : g.D0;
+  const uint32_t d1 = j2 ? g.D3 : j1 ? g.D2 : g.D1;
+  const int s1 = j3 ? g.L : j2 ? g.S3 : j1 ? g.S2 : g.S1;
+  const int s2 = j2 ? g.L : j1 ? g.S3 : g.S2;
+  c.A1 = (uint32_t)c.q0 + d0;
+  c.A2 = (uint32_t)c.q0 + d1;
+  c.B = s1 - c.q0;
+  c.two = s1 < hi;
+  c.clip = c.q0 < 0 || c.q0 + 16 > g.L;
+  c.slow = q < hi && (c.A1 > g.lim || (c.two && (s2 < hi || c.A2 > g.lim)));
+  return c;
+}
+// The chunk from its (at most two) loads: one mask per dword in the common
+// case, byte masks at the frame's ends, byte loads in the rare slow case.
+__device__ __forceinline__ u32x4 tx_build(const TxSegs &g, const TxCut &c, const u32x4 &xa, const u32x4 &xb,
+                                          __amdgpu_buffer_rsrc_t rs) {
+  u32x4 v{0, 0, 0, 0};
+  if (!c.clip && !c.slow) {
+    // bytes [0, B) from xa, [B, 16) from xb
+    const uint32_t b = (uint32_t)min(max(c.B, 0), 16);
+    const uint64_t lo = b >= 8u ? ~0ull : (1ull << (8u * b)) - 1u;
+    const uint64_t hm = b <= 8u ? 0ull : b >= 16u ? ~0ull : (1ull << (8u * (b - 8u))) - 1u;
+    v.x = (xa.x & (uint32_t)lo) | (xb.x & ~(uint32_t)lo);
+    v.y = (xa.y & (uint32_t)(lo >> 32)) | (xb.y & ~(uint32_t)(lo >> 32));
+    v.z = (xa.z & (uint32_t)hm) | (xb.z & ~(uint32_t)hm);
+    v.w = (xa.w & (uint32_t)(hm >> 32)) | (xb.w & ~(uint32_t)(hm >> 32));
+  } else if (!c.slow) {
+    const int lo = max(c.q0, 0) - c.q0, hi = min(c.q0 + 16, g.L) - c.q0;
+    merge_bytes(v, xa, lo, min(c.B, hi));
+    if (c.two) merge_bytes(v, xb, c.B, hi);
+  } else {
+    for (int q = max(c.q0, 0); q < min(c.q0 + 16, g.L); ++q) {
+      const uint32_t d = q >= g.S3 ? g.D3 : q >= g.S2 ? g.D2 : q >= g.S1 ? g.D1 : g.D0;
+      put_byte(v, q - c.q0, __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(q + (int)d), 0, 0));
+    }
+  }
+  return v;
+}
+
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
   static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
@@ -1326,89 +1395,36 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       // segment e covers frame bytes [S[e], S[e+1]) (the last one: to len),
       // frame byte q sits at source offset q + Dl[e]
-      int S[kTxSeg + 2];
-      uint32_t Dl[kTxSeg];
-#pragma unroll
-      for (int e = 0; e < kTxSeg; ++e) {
-        S[e] = (uint32_t)e < m ? (int)s_seg[grp][e][0] : (int)len;
-        Dl[e] = (uint32_t)e < m ? s_seg[grp][e][1] : 0u;
-      }
-      S[kTxSeg] = S[kTxSeg + 1] = (int)len;
-#pragma unroll
-      for (int e = 0; e < kTxSeg; ++e) S[e] = min(S[e], (int)len);
+      static_assert(kTxSeg == 4, "segment registers S1..S3 / D0..D3");
+      auto seg_start = [&](uint32_t e) { return e < m ? min((int)s_seg[grp][e][0], (int)len) : (int)len; };
+      auto seg_delta = [&](uint32_t e) { return e < m ? s_seg[grp][e][1] : 0u; };
       const uint32_t nch = (h + len + 15u) >> 4;
       const uint32_t npass = (nch + G * U - 1) / (G * U);
       // Chunk ci of the frame, gathered.  Its bytes [max(q0, 0), min(q0 + 16,
       // len)) come from segment j (the one holding the first byte) and, when
-      // the chunk crosses a segment end, j + 1: two loads at most, issued by
-      // `issue`, merged by `build`.  A chunk touching three segments (an mbuf
-      // shorter than 16 bytes) or a load crossing the source buffer's ends is
-      // assembled byte by byte (rare).
-      struct Cut {
-        int q0, lo, mid, hi;  // frame bytes [lo, mid) from j, [mid, hi) from j + 1
-        int64_t A1, A2;
-        bool slow;
-      };
-      auto cut = [&](uint32_t ci) {
-        Cut c;
-        c.q0 = (int)(16u * ci) - (int)h;
-        c.lo = max(c.q0, 0);
-        c.hi = min(c.q0 + 16, (int)len);
-        uint32_t j = 0;
-#pragma unroll
-        for (int e = 1; e < kTxSeg; ++e) j += c.lo >= S[e] ? 1u : 0u;
-        int s1 = (int)len, s2 = (int)len;
-        uint32_t d0 = Dl[0], d1 = 0;
-#pragma unroll
-        for (int e = 0; e < kTxSeg; ++e) {
-          if ((uint32_t)e == j) {
-            d0 = Dl[e];
-            s1 = S[e + 1];
-            if (e + 1 < kTxSeg) {
-              d1 = Dl[e + 1];
-              s2 = S[e + 2];
-            }
-          }
-        }
-        c.mid = min(s1, c.hi);
-        c.A1 = (int64_t)c.q0 + (int64_t)(int32_t)d0;
-        c.A2 = (int64_t)c.q0 + (int64_t)(int32_t)d1;
-        const bool two = c.mid < c.hi;
-        c.slow = c.lo < c.hi &&
-                 ((two && s2 < c.hi) || c.A1 < 0 || c.A1 + 16 > (int64_t)t.src_bytes ||
-                  (two && (c.A2 < 0 || c.A2 + 16 > (int64_t)t.src_bytes)));
-        return c;
-      };
-      auto issue = [&](uint32_t ci, u32x4 (&x)[2]) {
-        const Cut c = cut(ci);
-        const bool ok1 = c.lo < c.hi && !c.slow, ok2 = ok1 && c.mid < c.hi;
-        x[0] = ld16(rs, ok1 ? (uint32_t)c.A1 : kOOB);
-        x[1] = ld16(rs, ok2 ? (uint32_t)c.A2 : kOOB);
-      };
-      auto build = [&](uint32_t ci, const u32x4 (&x)[2]) {
-        const Cut c = cut(ci);
-        u32x4 v{0, 0, 0, 0};
-        if (!c.slow) {
-          merge_bytes(v, x[0], c.lo - c.q0, c.mid - c.q0);
-          merge_bytes(v, x[1], c.mid - c.q0, c.hi - c.q0);
-        } else {
-          for (int q = c.lo; q < c.hi; ++q) {
-            uint32_t d = Dl[0];
-#pragma unroll
-            for (int e = 1; e < kTxSeg; ++e) d = q >= S[e] ? Dl[e] : d;
-            put_byte(v, q - c.q0, ld_byte(rs, (uint32_t)(q + (int)d)));
-          }
-        }
-        return v;
-      };
+      // the chunk crosses a segment end at frame byte q0 + B, from j + 1: two
+      // loads at most (`issue`), one v_bfi per dword to merge them (`build`).
+      // Chunks clipped by the frame's ends merge with byte masks; a chunk
+      // touching three segments (an mbuf shorter than 16 bytes) or whose load
+      // would cross the source buffer's ends is assembled byte by byte (rare).
+      const int L = (int)len;
+      const int S1 = seg_start(1), S2 = seg_start(2), S3 = seg_start(3);
+      const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
+      const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
+      const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
       u32x4 held{0, 0, 0, 0};
       for (uint32_t p = 0; p < npass; ++p) {
-        u32x4 x[U][2];
+        u32x4 xa[U], xb[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) issue(p * (G * U) + u * G + lane, x[u]);
+        for (int u = 0; u < U; ++u) {
+          const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
+          xa[u] = ld16(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
+          xb[u] = ld16(rs, c.two && !c.slow ? c.A2 : kOOB);
+        }
         u32x4 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = build(p * (G * U) + u * G + lane, x[u]);
+        for (int u = 0; u < U; ++u)
+          v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
