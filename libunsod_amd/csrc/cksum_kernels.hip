@@ -1400,14 +1400,8 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
       auto seg_delta = [&](uint32_t e) { return e < m ? s_seg[grp][e][1] : 0u; };
       const uint32_t nch = (h + len + 15u) >> 4;
       const uint32_t npass = (nch + G * U - 1) / (G * U);
-      // Chunk ci of the frame, gathered.  Its bytes [max(q0, 0), min(q0 + 16,
-      // len)) come from segment j (the one holding the first byte) and, when
-      // the chunk crosses a segment end at frame byte q0 + B, from j + 1: two
-      // loads at most (`issue`), one v_bfi per dword to merge them (`build`).
-      // Chunks clipped by the frame's ends merge with byte masks; a chunk
-      // touching three segments (an mbuf shorter than 16 bytes) or whose load
-      // would cross the source buffer's ends is assembled byte by byte (rare).
-      const int L = (int)len;
+      // Chunk ci of the frame is gathered from at most two loads (tx_cut,
+      // tx_build above).
       const int S1 = seg_start(1), S2 = seg_start(2), S3 = seg_start(3);
       const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
       const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
@@ -1753,17 +1747,21 @@ struct Plan {
 };
 
 Plan verify_plan(const Desc &d, uint32_t max_len) {
-  static const int pu = [] {
+  // chunks per lane per pass of the flat-run kernel: 8 for packed mixed
+  // lengths, 4 for dense minimum-size slots (profiles/packed_u_r01.jsonl);
+  // MI_CKSUM_PACKED_U overrides
+  static const int pu_env = [] {
     const char *e = getenv("MI_CKSUM_PACKED_U");
-    const int u = e ? atoi(e) : 4;
-    return u == 8 || u == 16 ? u : 4;
+    const int u = e ? atoi(e) : 0;
+    return u == 4 || u == 8 || u == 16 ? u : 0;
   }();
   // the flat-run kernel: hinted packed layouts, and fixed slots that hold
   // little besides the datagram (minimum-size frames: streaming the whole slot
   // costs no more HBM traffic than reading the datagrams' own lines)
   const bool dense_slots = !d.offs && !d.lens && d.stride &&
                            d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
-  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) return {kPlanRun, {0, 0}, pu};
+  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g)
+    return {kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
   if (!d.lens || g_tune.g || max_len < kClassEdges[1]) return {kPlanShape, pick_shape(max_len), 0};
   return {kPlanClasses, {0, 0}, 0};
 }

@@ -89,6 +89,6 @@ def test_verify_plan_needs_no_gpu():
     assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=14, fixed_len=46)) == "k_ipv4_verify_packed<4>"
     offs = torch.arange(100, dtype=torch.int64) * 300
     lens = torch.full((100,), 280, dtype=torch.int32)
-    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<4>"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8>"
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens)) == "k_ipv4_verify x length classes"
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens // 4)) == "k_ipv4_verify<1,8>"
