@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--streams", type=int, default=2, help="streams the steps alternate over")
+    ap.add_argument("--submit", default="launch", choices=["graph", "launch"],
+                    help="launch: K host launches from native code; graph: the same K launches as one cached "
+                         "hipGraph (measured slower for 1500 B: profiles/submit_r01.jsonl)")
     ap.add_argument("--settle", type=float, default=0.3,
                     help="untimed warm-up lasts at least this many seconds (GPU clock settle)")
     return ap.parse_args()
@@ -137,8 +140,9 @@ def main():
 
     nst = max(1, args.streams)
     tw = time.perf_counter()
+    use_graph = args.submit == "graph"
     if args.warmup:
-        mi.ipv4_verify_repeat(batches, outs, args.warmup, nstreams=nst, timing="none")
+        mi.ipv4_verify_repeat(batches, outs, args.warmup, nstreams=nst, timing="none", graph=use_graph)
     torch.cuda.synchronize()
     # Settle: the first ~0.1 s of back-to-back launches run up to 20 % slower
     # (clock / translation warm-up; profiles/warmup_r01.jsonl: 40 warmup steps ->
@@ -146,20 +150,25 @@ def main():
     # the warmup phase has lasted `--settle` seconds, whatever W is.
     settle_steps = 0
     while time.perf_counter() - tw < args.settle:
-        mi.ipv4_verify_repeat(batches, outs, 500, nstreams=nst, timing="none")
+        mi.ipv4_verify_repeat(batches, outs, 500, nstreams=nst, timing="none", graph=use_graph)
         settle_steps += 500
     cfg["settle_steps"] = settle_steps
+    cfg["submit"] = args.submit
+    if use_graph:  # instantiate the timed region's graph (K passes) before timing it
+        mi.ipv4_verify_repeat(batches, outs, args.steps, nstreams=nst, timing="none", graph=True)
 
     # ------------------------------------------------------- timed region
     # K launches issued back to back from native code (libmicksum), alternating
     # over `nst` non-blocking streams so that a launch's ramp-up overlaps its
     # predecessor's drain; a hipEvent pair per stream brackets the region.
+    # --submit graph: the same K launches captured once into a hipGraph
+    # (instantiated above, outside the timed region) and replayed.
     K = args.steps
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    span_us = mi.ipv4_verify_repeat(batches, outs, K, nstreams=nst, timing="region")
+    span_us = mi.ipv4_verify_repeat(batches, outs, K, nstreams=nst, timing="region", graph=use_graph)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:

@@ -269,6 +269,10 @@ int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *c
 #define MI_TIME_NONE     0u
 #define MI_TIME_REGION   1u
 #define MI_TIME_PER_PASS 2u
+/* OR'ed into timing (with NONE or REGION): submit the passes as one hipGraph
+ * (stream capture of the same launches, instantiated on first use and cached
+ * per launch sequence), so consecutive passes cost no host launch overhead. */
+#define MI_REPEAT_GRAPH  0x100u
 int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip,
                                 uint16_t *const *l4, uint8_t *const *status, uint32_t steps,
                                 uint32_t nstreams, uint32_t timing, float *kernel_us,

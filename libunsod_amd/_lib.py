@@ -25,6 +25,7 @@ MI_BATCH_HOST_STAGED = 4
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2
+MI_REPEAT_GRAPH = 0x100
 MI_CHAIN_SKIP = 0
 MI_CHAIN_PSEUDO = 1
 MI_CSUM_IP_CHECKED = 0x100

@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_REPEAT_GRAPH, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -312,15 +312,19 @@ def tx_copy(tb: TxBatch, *, status=None, stream=None):
     return status
 
 
-def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str = "region"):
+def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str = "region",
+                       graph: bool = False):
     """Launch ``steps`` verify passes back to back from native code: pass k over
     batches[k % nb] into outs[k % nb] = dict(ip, l4, status), on the library's
     k % nstreams-th non-blocking stream.  Synchronous.
 
     timing="none" -> None; "region" -> GPU span of all passes in us (one
     hipEvent pair around the region per stream); "pass" -> (per-pass durations
-    in us, span in us), events around every pass."""
+    in us, span in us), events around every pass.  ``graph``: submit the passes
+    as one cached hipGraph (MI_REPEAT_GRAPH; "none" / "region" only)."""
     mode = {"none": MI_TIME_NONE, "region": MI_TIME_REGION, "pass": MI_TIME_PER_PASS}[timing]
+    if graph:
+        mode |= MI_REPEAT_GRAPH
     nb = len(batches)
     arr = (PktBatchC * nb)(*[b.c for b in batches])
     VP = C.c_void_p * nb
@@ -330,6 +334,7 @@ def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str
     check("mi_cksum_ipv4_verify_repeat",
           load().mi_cksum_ipv4_verify_repeat(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], steps, nstreams,
                                              mode, us, C.byref(span)))
+    mode &= ~MI_REPEAT_GRAPH
     if mode == MI_TIME_NONE:
         return None
     if mode == MI_TIME_REGION:

@@ -1408,6 +1408,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
       const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
       u32x4 held{0, 0, 0, 0};
       for (uint32_t p = 0; p < npass; ++p) {
+        u32x4 v[U];
         u32x4 xa[U], xb[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1415,7 +1416,6 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
           xa[u] = ld16(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
           xb[u] = ld16(rs, c.two && !c.slow ? c.A2 : kOOB);
         }
-        u32x4 v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
           v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
@@ -1589,6 +1589,16 @@ struct ThreadCtx {
   static constexpr int kMaxRep = 8;
   hipStream_t rstream[kMaxRep] = {};
   hipEvent_t rgate = nullptr;
+  // MI_REPEAT_GRAPH: instantiated graphs of K passes, keyed by their launches
+  struct RepGraph {
+    uint64_t key = 0;
+    uint32_t steps = 0, nstreams = 0;
+    hipGraphExec_t exec = nullptr;
+  };
+  static constexpr int kGraphs = 4;
+  RepGraph rgraph[kGraphs];
+  uint32_t rgraph_next = 0;
+  hipEvent_t rfork = nullptr, rjoin[kMaxRep] = {};
   hipEvent_t *ev = nullptr;
   uint32_t nev = 0;
 };
@@ -2016,9 +2026,77 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
     }
   }
   if (!c.rgate) HIP_TRY(hipEventCreateWithFlags(&c.rgate, hipEventDisableTiming));
+  const bool graph = timing & MI_REPEAT_GRAPH;
+  timing &= ~MI_REPEAT_GRAPH;
+  if (graph && timing == MI_TIME_PER_PASS) return set_err(-EINVAL, "MI_REPEAT_GRAPH times the region only");
   // order after everything already queued on the legacy default stream
   HIP_TRY(hipEventRecord(c.rgate, nullptr));
   for (uint32_t q = 0; q < nstreams; ++q) HIP_TRY(hipStreamWaitEvent(c.rstream[q], c.rgate, 0));
+  if (graph) {
+    // The K passes as one hipGraph: the same launches on the same stream
+    // pattern (captured: stream 0 forks to the others and joins them), so a
+    // pass costs no host launch overhead.  Instantiated once per launch
+    // sequence and kept (a small per-thread cache).
+    uint64_t key = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+      const uint8_t *q = (const uint8_t *)p;
+      for (size_t i = 0; i < n; ++i) key = (key ^ q[i]) * 1099511628211ull;
+    };
+    mix(d, sizeof(Desc) * nb);
+    mix(ml, sizeof(uint32_t) * nb);
+    for (uint32_t k = 0; k < nb; ++k) {
+      const void *o[3] = {ip ? ip[k] : nullptr, l4 ? l4[k] : nullptr, status ? status[k] : nullptr};
+      mix(o, sizeof o);
+    }
+    mix(&g_tune, sizeof g_tune);
+    ThreadCtx::RepGraph *gr = nullptr;
+    for (auto &e : c.rgraph)
+      if (e.exec && e.key == key && e.steps == steps && e.nstreams == nstreams) gr = &e;
+    if (!gr) {
+      if (!c.rfork) {
+        HIP_TRY(hipEventCreateWithFlags(&c.rfork, hipEventDisableTiming));
+        for (int q = 0; q < ThreadCtx::kMaxRep; ++q) HIP_TRY(hipEventCreateWithFlags(&c.rjoin[q], hipEventDisableTiming));
+      }
+      HIP_TRY(hipStreamSynchronize(c.rstream[0]));
+      HIP_TRY(hipStreamBeginCapture(c.rstream[0], hipStreamCaptureModeThreadLocal));
+      HIP_TRY(hipEventRecord(c.rfork, c.rstream[0]));
+      for (uint32_t q = 1; q < nstreams; ++q) HIP_TRY(hipStreamWaitEvent(c.rstream[q], c.rfork, 0));
+      for (uint32_t k = 0; k < steps && !rc; ++k) {
+        const uint32_t j = k % nb;
+        rc = launch_verify(d[j], ml[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
+                           status ? status[j] : nullptr, nullptr, c.rstream[k % nstreams]);
+      }
+      for (uint32_t q = 1; q < nstreams; ++q) {
+        HIP_TRY(hipEventRecord(c.rjoin[q], c.rstream[q]));
+        HIP_TRY(hipStreamWaitEvent(c.rstream[0], c.rjoin[q], 0));
+      }
+      hipGraph_t g = nullptr;
+      HIP_TRY(hipStreamEndCapture(c.rstream[0], &g));
+      if (rc) {
+        (void)hipGraphDestroy(g);
+        return rc;
+      }
+      gr = &c.rgraph[c.rgraph_next];
+      c.rgraph_next = (c.rgraph_next + 1) % ThreadCtx::kGraphs;
+      if (gr->exec) (void)hipGraphExecDestroy(gr->exec);
+      gr->exec = nullptr;
+      HIP_TRY(hipGraphInstantiate(&gr->exec, g, nullptr, nullptr, 0));
+      (void)hipGraphDestroy(g);
+      gr->key = key;
+      gr->steps = steps;
+      gr->nstreams = nstreams;
+      HIP_TRY(hipGraphUpload(gr->exec, c.rstream[0]));
+      HIP_TRY(hipStreamSynchronize(c.rstream[0]));
+    }
+    if (timing == MI_TIME_REGION) HIP_TRY(hipEventRecord(c.ev[0], c.rstream[0]));
+    HIP_TRY(hipGraphLaunch(gr->exec, c.rstream[0]));
+    if (timing == MI_TIME_REGION) HIP_TRY(hipEventRecord(c.ev[2], c.rstream[0]));
+    HIP_TRY(hipStreamSynchronize(c.rstream[0]));
+    float span = 0.f;
+    if (timing == MI_TIME_REGION) HIP_TRY(hipEventElapsedTime(&span, c.ev[0], c.ev[2]));
+    if (span_us) *span_us = span * 1000.f;
+    return 0;
+  }
   if (timing == MI_TIME_REGION) {
     HIP_TRY(hipEventRecord(c.ev[0], c.rstream[0]));
     for (uint32_t q = 1; q < nstreams; ++q) HIP_TRY(hipStreamWaitEvent(c.rstream[q], c.ev[0], 0));

@@ -292,6 +292,15 @@ def test_deterministic_and_stream_async():
     assert mi.ipv4_verify_repeat([b], outs, 6, nstreams=3, timing="region") > 0
     for k in ("ip", "l4", "status"):
         assert np.array_equal(cpu(outs[0][k]), cpu(r1[k]))
+    # the same passes as a cached hipGraph (MI_REPEAT_GRAPH): same outputs, replayable
+    for k in ("ip", "l4", "status"):
+        outs[0][k].fill_(3)
+    assert mi.ipv4_verify_repeat([b], outs, 10, nstreams=2, timing="region", graph=True) > 0
+    for k in ("ip", "l4", "status"):
+        assert np.array_equal(cpu(outs[0][k]), cpu(r1[k]))
+    buf[142 + 5 * 2176 + 700] ^= 1  # the graph reads the batch afresh on every replay
+    assert mi.ipv4_verify_repeat([b], outs, 10, nstreams=2, timing="none", graph=True) is None
+    assert int((outs[0]["status"] != 0).sum().item()) == 1
 
 
 SHAPES = [(1, 4), (1, 8), (4, 1), (4, 2), (4, 4), (8, 2), (8, 4), (8, 8), (8, 12), (16, 2), (16, 4), (16, 6),
