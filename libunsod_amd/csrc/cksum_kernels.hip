@@ -1780,7 +1780,12 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
                   uint32_t *bad, hipStream_t s) {
   const Plan pl = verify_plan(d, max_len);
   if (pl.kind == kPlanRun) {
-    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+    static const int run_cap = [] {
+      const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 ? v : 16384;
+    }();
+    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap;
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
     if (blocks > (uint64_t)cap) blocks = cap;
     const dim3 grid(blocks ? (unsigned)blocks : 1u);
