@@ -780,6 +780,59 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
   }
 }
 
+// RX verify of minimum-size frames in 64-byte slots (stride 64, the datagram
+// inside its slot, starting < 16 bytes in: the 64 B config, 46 B datagrams at
+// +14).  A wave owns 64 consecutive slots: four fully coalesced 1 KiB
+// wave-loads bring the 4 KiB in, a transpose through LDS (4 KiB per wave)
+// hands lane k its own slot's four chunks, and the lane folds its datagram
+// directly -- no scan, no per-datagram header / tail reloads (which cost the
+// flat-run kernel four scattered 16-byte L2 requests per datagram).
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                               uint8_t *st_out, uint32_t *bad) {
+  __shared__ u32x4 s_slot[kBlock / 64][256];
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t h = (uint32_t)(d.first_off & 63u), slot0 = (uint32_t)(d.first_off - h);
+  const uint32_t flen = pkt_len(d, 0);
+  const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
+  u32x4 *sl = s_slot[wv];
+  for (uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u; p0 < d.n; p0 += rstride) {
+    const uint32_t base = slot0 + 64u * p0, nslot = min(64u, d.n - p0);
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t c = 64u * u + lane;  // chunk of the range: slot c / 4
+      v[u] = ld16(r, c < 4u * nslot ? base + 16u * c : kOOB);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sl[64u * u + lane] = v[u];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u32x4 w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = sl[4u * lane + j];
+    __builtin_amdgcn_wave_barrier();  // reads done before the next range rewrites the slots
+    const uint32_t i = p0 + lane;
+    if (i < d.n) {
+      const uint32_t off = base + 64u * lane + h;
+      const IpHdr ih = parse_ipv4<1, 4>(w, h);
+      const bool odd = h & 1u;
+      const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+      const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+      const uint32_t hend = hdr_ok ? ih.hl : 0u;
+      const uint32_t lend = l4_ok ? ih.iplen : hend;
+      uint32_t total = 0, hdr = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        total += range_sum(w[j], 16 * j - (int)h, 0, (int)lend);
+        hdr += range_sum(w[j], 16 * j - (int)h, 0, (int)hend);
+      }
+      verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r, off);
+    }
+  }
+}
+
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
 // (ip_output.c:667-672).
 template <int G, int U>
@@ -1749,7 +1802,7 @@ int launch_verify_shape(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uin
 constexpr uint32_t kClassEdges[] = {0u, 99u, 739u, 2019u, ~0u};
 
 // Which verify kernel a batch gets.
-enum PlanKind { kPlanRun, kPlanShape, kPlanClasses };
+enum PlanKind { kPlanRun, kPlanShape, kPlanClasses, kPlanSlot64 };
 struct Plan {
   PlanKind kind;
   Shape shape;  // kPlanShape
@@ -1770,6 +1823,10 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
   // costs no more HBM traffic than reading the datagrams' own lines)
   const bool dense_slots = !d.offs && !d.lens && d.stride &&
                            d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
+  // minimum-size frames in 64-byte slots: one lane per slot after an LDS transpose
+  if (dense_slots && d.stride == 64u && (d.first_off & 63u) < 16u && (d.first_off & 63u) + d.fixed_len <= 64u &&
+      !g_tune.g && !pu_env)
+    return {kPlanSlot64, {0, 0}, 0};
   if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g)
     return {kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
   if (!d.lens || g_tune.g || max_len < kClassEdges[1]) return {kPlanShape, pick_shape(max_len), 0};
@@ -1795,6 +1852,14 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
       hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
     else
       hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+    return launched();
+  }
+  if (pl.kind == kPlanSlot64) {
+    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+    uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 slots per wave
+    if (blocks > (uint64_t)cap) blocks = cap;
+    hipLaunchKernelGGL(k_ipv4_verify_slot64, dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d, ip, l4,
+                       st, bad);
     return launched();
   }
   if (pl.kind == kPlanShape) return launch_verify_shape(d, pl.shape, ip, l4, st, bad, s);
@@ -1979,6 +2044,8 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
     snprintf(buf, sizeof buf, "k_ipv4_verify_packed<%d>", pl.run_u);
   else if (pl.kind == kPlanShape)
     snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);
+  else if (pl.kind == kPlanSlot64)
+    snprintf(buf, sizeof buf, "k_ipv4_verify_slot64");
   else
     snprintf(buf, sizeof buf, "k_ipv4_verify x length classes");
   return buf;

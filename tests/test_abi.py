@@ -86,7 +86,8 @@ def test_verify_plan_needs_no_gpu():
     import libunsod_amd as mi
     buf = torch.zeros(1 << 20, dtype=torch.uint8)
     assert mi.verify_plan(mi.PktBatch(buf, 100, stride=2176, first_off=142, fixed_len=1500)).startswith("k_ipv4_verify<")
-    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=14, fixed_len=46)) == "k_ipv4_verify_packed<4>"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=14, fixed_len=46)) == "k_ipv4_verify_slot64"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=30, fixed_len=46)) == "k_ipv4_verify_packed<4>"
     offs = torch.arange(100, dtype=torch.int64) * 300
     lens = torch.full((100,), 280, dtype=torch.int32)
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8>"

@@ -499,3 +499,48 @@ def test_rx_offload_flags(layout):
     assert np.array_equal(((fl & CSUM_IP_VALID) == 0)[chk], (ip_o != 0)[chk])
     dv = (fl & CSUM_DATA_VALID) != 0
     assert np.array_equal((cd ^ 0xFFFF)[dv], l4_o[dv].astype(np.uint32))
+
+
+@pytest.mark.parametrize("first", [14, 2, 7, 30])
+def test_slot64_edge_cases(first):
+    """Minimum-size frames in 64-byte slots (k_ipv4_verify_slot64): malformed
+    headers, IP options, Ethernet padding past ip_len, UDP / ICMP / IGMP,
+    fragments and corrupted bytes at odd and even starts -- verify, demux
+    verify and RX offload flags all equal the oracle."""
+    rng = np.random.default_rng(first)
+    n, L, stride = 6000, 46, 64
+    proto = rng.choice([6, 17, 1, 2], n)
+    hl = rng.choice([20, 20, 20, 24], n)
+    b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, proto=proto, hl=hl, seed=first + 1)
+    host = b0["buf"]
+    _, h = aligned(host)
+    ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+    for i in rng.choice(n, 600, replace=False):
+        p = first + int(i) * stride
+        k = int(rng.integers(0, 6))
+        if k == 0:
+            h[p] = 0x40 | int(rng.integers(0, 16))                 # any hl, incl. < 20 and > flen
+        elif k == 1:
+            v = int(rng.integers(0, 80))                          # ip_len below, at or past the frame
+            h[p + 2], h[p + 3] = v >> 8, v & 0xFF
+        elif k == 2:
+            h[p + 6] = 0x20                                       # a fragment
+        else:
+            h[p + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(8)))
+    buf = dev_tensor(h)
+    b = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
+    assert mi.verify_plan(b) == ("k_ipv4_verify_slot64" if first < 16 else "k_ipv4_verify_packed<4>")
+    r = mi.ipv4_verify(b, bad_count=True)
+    ip, l4, st = ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+    assert np.array_equal(cpu(r["ip"]), ip) and np.array_equal(cpu(r["l4"]), l4)
+    assert np.array_equal(cpu(r["status"]), st) and int(r["bad"].item()) == int((st != 0).sum())
+    bd = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L, demux=True)
+    rd = mi.ipv4_verify(bd)
+    ipd, l4d, std = ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L, demux=True)
+    assert np.array_equal(cpu(rd["l4"]), l4d) and np.array_equal(cpu(rd["status"]), std)
+    from oracle.pyoracle import rx_offload_flags
+    offs = first + np.arange(n, dtype=np.int64) * stride
+    fl, cd = rx_offload_flags(h, offs, np.full(n, L), ip, l4, st)
+    ro = mi.rx_offload(b)
+    assert np.array_equal(cpu(ro["flags"]).view(np.uint32), fl)
+    assert np.array_equal(cpu(ro["data"]).view(np.uint32), cd)
