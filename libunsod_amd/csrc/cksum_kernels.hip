@@ -657,6 +657,9 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
+#ifndef MI_RUN_CAPTURE
+#define MI_RUN_CAPTURE 1  // flat-run kernel: header windows from the streamed passes (0: reload them)
+#endif
 #ifdef MI_EXP_LB
 #define PACKED_BOUNDS __launch_bounds__(kBlock, MI_EXP_LB)
 #else
@@ -668,6 +671,9 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
                                                                uint32_t *bad) {
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[kBlock / 64][W];
+#if MI_RUN_CAPTURE
+  __shared__ u32x4 s_c[kBlock / 64][W];  // the pass's chunks: header windows / last chunks come from here
+#endif
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
@@ -718,9 +724,16 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
       const uint32_t cs = st >> 4, ce = en >> 4, h = st & 15u, t = en & 15u;
       // this datagram's header window and last (partial) chunk
       u32x4 hv[3], tv;
+#if MI_RUN_CAPTURE
+      // captured from the run's own passes as they stream by (LDS), not reloaded
+#pragma unroll
+      for (int k = 0; k < 3; ++k) hv[k] = u32x4{0, 0, 0, 0};
+      tv = u32x4{0, 0, 0, 0};
+#else
 #pragma unroll
       for (int k = 0; k < 3; ++k) hv[k] = ld16_keep(r, act ? r0 + 16u * (cs + k) : kOOB);
       tv = ld16_keep(r, act && t ? r0 + 16u * ce : kOOB);
+#endif
       uint32_t carry = 0, qs = 0, qe = 0;
       for (uint32_t cb = 0;;) {
 #pragma unroll
@@ -728,6 +741,9 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
           const uint32_t x = sum4(v[u]);  // chunks past the run load as zeros
           const uint32_t inc = wave_scan(x);
           sq[64u * u + lane] = carry + inc - x;
+#if MI_RUN_CAPTURE
+          s_c[wv][64u * u + lane] = v[u];
+#endif
           carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -735,6 +751,14 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (cs - cb < W) qs = sq[cs - cb];
         if (ce - cb < W) qe = sq[ce - cb];
+#if MI_RUN_CAPTURE
+        if (act) {
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            if (cs + k - cb < W) hv[k] = s_c[wv][cs + k - cb];
+          if (t && ce - cb < W) tv = s_c[wv][ce - cb];
+        }
+#endif
         cb += W;
         if (cb >= nch) break;
 #pragma unroll
