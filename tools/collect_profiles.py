@@ -37,7 +37,8 @@ def main():
         # the verify kernel that dominates the trace (the bench line names it too)
         stats = open(os.path.join(kt, "run_kernel_stats.csv")).read().splitlines()[1:]
         kern = max((l for l in stats if "k_ipv4_verify" in l), key=lambda l: int(l.rsplit('",', 1)[1].split(",")[1]))
-        kern = kern.split('"')[1].replace("void (anonymous namespace)::", "").split("((anonymous")[0]
+        kern = kern.split('"')[1].split("((anonymous")[0]
+        kern = kern.replace("void (anonymous namespace)::", "").replace("(anonymous namespace)::", "")
         short = kern.split("<")[0]
         shutil.copy(os.path.join(kt, "run_kernel_stats.csv"),
                     os.path.join(prof, f"rocprof_kernel_stats_{c}_{a.round}.csv"))
