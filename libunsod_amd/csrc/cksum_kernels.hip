@@ -614,6 +614,64 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 // is not falls back to one lane per datagram.  Bytes past ip_len (Ethernet
 // padding) are subtracted afterwards and L4 = total - header, as in ipv4_sums.
 
+// TX stores of one datagram from its header / L4 sums (ipv4_sums<TX>):
+// in_delayed_cksum (ip_output.c:958-983) or, with MI_BATCH_DEMUX, the
+// small-header senders; then ip_sum = in_cksum(m, hlen) (:667-672).
+__device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen, bool odd,
+                                               const IpHdr &ih, bool hdr_ok, bool do_l4, bool demux,
+                                               uint32_t sum_h, uint32_t sum_l) {
+  if (!(hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen)) return;  // malformed: untouched
+  const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
+  if (do_l4 && demux && (ip_off & 0x3fffu)) {
+    // a fragment: ip_fragment summed the datagram before cutting it
+  } else if (do_l4 && (ih.proto == 6u || ih.proto == 17u)) {
+    uint32_t sl = fold16(sum_l);
+    if (odd) sl = swap16(sl);
+    uint32_t c = ~sl & 0xffffu;
+    if (ih.proto == 17u && c == 0u) c = 0xffffu;
+    const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
+    if (at + 2u <= flen) {
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+    }
+  } else if (do_l4) {
+    // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
+    const bool carp = ih.proto == 112u;
+    const uint32_t plen = ih.iplen - ih.hl, span = carp ? 36u : plen;
+    if (plen >= (carp ? 36u : 8u)) {
+      const uint32_t at = ih.hl + (carp ? 6u : 2u);
+      const uint32_t b0 = ld_byte(r, off + at), b1 = ld_byte(r, off + at + 1u);
+      const uint32_t field = odd ? (b0 << 8) + b1 : b0 + (b1 << 8);  // abs lanes, at even
+      uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l) - field);
+      if (odd) sl = swap16(sl);
+      const uint32_t c = ~sl & 0xffffu;
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+    }
+  }
+  uint32_t sh = fold16(sum_h);
+  if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
+  const uint32_t c = ~sh & 0xffffu;
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + 11u, 0, 0);
+}
+
+// One span's output (k_span's epilogue): the absolute-lane sum S of its bytes,
+// swapped to stream lanes when the span starts odd (in_cksum.c:222-225), plus
+// the seeds, folded and complemented.
+__device__ __forceinline__ void span_store(uint32_t i, uint32_t off, uint32_t len, bool swap, uint32_t S,
+                                           const SpanSeeds &s, uint16_t *out) {
+  (void)off;
+  uint64_t sum = fold16(S);
+  if (swap) sum = swap16((uint32_t)sum);
+  if (s.seeds) sum += s.seeds[i];
+  if (s.src) {
+    const uint32_t pl = s.plens ? s.plens[i] : len;
+    sum += (uint64_t)s.src[i] + s.dst[i] + ((uint32_t)s.proto[i] << 8) + swap16(pl & 0xffffu);
+  }
+  out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+}
+
 // Inclusive prefix sum over the wave: row shifts inside 16-lane rows, then
 // the row_bcast:15 / row_bcast:31 carries across rows.
 __device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
@@ -665,10 +723,14 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 #else
 #define PACKED_BOUNDS __launch_bounds__(kBlock)
 #endif
-template <int U>
+// MODE: 0 RX verify; 1 TX finalize in place (finalize_store); 2 span folds
+// (mi_cksum_span_batch: out = ip_out, in_cksum_skip / pseudo-header seeds).
+template <int U, int MODE = 0>
 __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
                                                                uint16_t *l4_out, uint8_t *st_out,
-                                                               uint32_t *bad) {
+                                                               uint32_t *bad, SpanSeeds sp,
+                                                               uint32_t abs_lanes) {
+  constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[kBlock / 64][W];
 #if MI_RUN_CAPTURE
@@ -688,7 +750,8 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
     const uint32_t i = p0 + lane;
     const bool act = i < d.n;
     const uint32_t end = act ? off + flen : 0u;
-    const bool sane = !act || (off < kOOB && end >= off && end <= d.bytes);
+    // (a span's sum must stay below 2^32 for Q(end) - Q(start) to be exact)
+    const bool sane = !act || (off < kOOB && end >= off && end <= d.bytes && (!SPAN || flen <= 65535u));
     const uint32_t r0 = wave_min(act ? off : ~0u) & ~15u;
     const uint32_t r1 = wave_max(end);
     const uint32_t nch = (r1 - r0 + 15u) >> 4;
@@ -709,15 +772,24 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
     }
     if (!packed) {
       // not packed: one lane per datagram
-      if (act) {
+      if (act && SPAN) {
+        uint64_t acc = 0;  // one lane walks the span (64-bit: any length)
+        for (uint32_t c = off & ~15u; c < off + flen; c += 16u)
+          acc += range_sum(ld16(r, c), (int)(c - off), 0, (int)flen);
+        span_store(i, off, flen, (((uintptr_t)d.base + off) & 1u) && !abs_lanes, fold16_64(acc), sp, ip_out);
+      } else if (act) {
         u32x4 w[4];
         issue_first<1, 4>(r, off, flen, 0, w);
         IpHdr ih;
         bool hdr_ok, l4_ok;
         uint32_t sum_h, sum_l;
-        ipv4_sums<1, 4, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l);
-        verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
-                     l4_out, st_out, bad, d, r, off);
+        const bool demux = d.flags & MI_BATCH_DEMUX;
+        ipv4_sums<1, 4, TX>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l, demux);
+        if constexpr (TX)
+          finalize_store(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, demux, sum_h, sum_l);
+        else
+          verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
+                       l4_out, st_out, bad, d, r, off);
       }
     } else {
       const uint32_t st = act ? off - r0 : 0u, en = act ? end - r0 : 0u;
@@ -769,31 +841,44 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
         __builtin_amdgcn_wave_barrier();  // lookups done before the next pass rewrites s_q
       }
       if (ce >= nch) qe = carry;  // end on the run's last chunk boundary
-      if (act) {
+      if (act && SPAN) {
+        const uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(hv[0], 0, 0, (int)h));
+        span_store(i, off, flen, (h & 1u) && !abs_lanes, total, sp, ip_out);
+      } else if (act) {
         const IpHdr ih = parse_ipv4<1, 3>(hv, h);
         const bool odd = h & 1u;
+        const bool demux = d.flags & MI_BATCH_DEMUX;
         const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-        const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+        const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+        // TX: only the protocols whose senders sum their message (ipv4_sums<TX>)
+        const bool l4_ok = TX ? len_ok && (ih.proto == 6u || ih.proto == 17u ||
+                                           (demux && (ih.proto == 1u || ih.proto == 2u || ih.proto == 112u)))
+                              : len_ok;
         const uint32_t hend = hdr_ok ? ih.hl : 0u;
         const uint32_t lend = l4_ok ? ih.iplen : hend;
         // bytes [off, off + flen) = Q(end) - Q(start)
         uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(hv[0], 0, 0, (int)h));
-        uint32_t hdr = 0;
+        uint32_t hdr = 0, field = 0;  // field: the ip_sum bytes (TX sums the header with them as 0)
         if (hend == 20u) {
           hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
                 abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+          if (TX) field = abs_halves(ih.w[2] & 0xffff0000u, odd);
         } else if (hend > 20u) {  // IP options (rare): up to 60 header bytes, 5 chunks
           for (uint32_t k = 0; k < 5; ++k) {
             const u32x4 x = k < 3 ? hv[k] : ld16(r, (off & ~15u) + 16u * k);
             hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
+            if (TX) field += range_sum(x, (int)(16u * k) - (int)h, 10, 12);
           }
         }
         if (lend < flen) {  // bytes past ip_len (Ethernet padding, malformed): rare
           for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
             total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
         }
-        verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r,
-                     off);
+        if constexpr (TX)
+          finalize_store(r, off, flen, odd, ih, hdr_ok, l4_ok, demux, hdr - field, total - hdr);
+        else
+          verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r,
+                       off);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -869,43 +954,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
     uint32_t sum_h, sum_l;
     const bool demux = d.flags & MI_BATCH_DEMUX;
     ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux);
-    const bool ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-    if (lane == 0 && ok) {
-      const bool odd = ((uintptr_t)d.base + off) & 1u;
-      const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
-      if (do_l4 && demux && (ip_off & 0x3fffu)) {
-        // a fragment: ip_fragment summed the datagram before cutting it
-      } else if (do_l4 && (ih.proto == 6u || ih.proto == 17u)) {
-        uint32_t sl = fold16(sum_l);
-        if (odd) sl = swap16(sl);
-        uint32_t c = ~sl & 0xffffu;
-        if (ih.proto == 17u && c == 0u) c = 0xffffu;
-        const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
-        if (at + 2u <= flen) {
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
-        }
-      } else if (do_l4) {
-        // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
-        const bool carp = ih.proto == 112u;
-        const uint32_t plen = ih.iplen - ih.hl, span = carp ? 36u : plen;
-        if (plen >= (carp ? 36u : 8u)) {
-          const uint32_t at = ih.hl + (carp ? 6u : 2u);
-          const uint32_t b0 = ld_byte(r, off + at), b1 = ld_byte(r, off + at + 1u);
-          const uint32_t field = odd ? (b0 << 8) + b1 : b0 + (b1 << 8);  // abs lanes, at even
-          uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l) - field);
-          if (odd) sl = swap16(sl);
-          const uint32_t c = ~sl & 0xffffu;
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
-        }
-      }
-      uint32_t sh = fold16(sum_h);
-      if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
-      const uint32_t c = ~sh & 0xffffu;
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + 11u, 0, 0);
-    }
+    if (lane == 0) finalize_store(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
   });
 }
 
@@ -1871,11 +1920,11 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     if (blocks > (uint64_t)cap) blocks = cap;
     const dim3 grid(blocks ? (unsigned)blocks : 1u);
     if (pl.run_u == 4)
-      hipLaunchKernelGGL((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+      hipLaunchKernelGGL((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     else if (pl.run_u == 16)
-      hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+      hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     else
-      hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad);
+      hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     return launched();
   }
   if (pl.kind == kPlanSlot64) {
@@ -1901,6 +1950,14 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
 
 int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd, uint16_t *out,
                 hipStream_t s) {
+  if ((d.flags & MI_BATCH_PACKED) && !g_tune.g) {  // packed mixed lengths: the flat run
+    uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+    if (blocks > (uint64_t)cap) blocks = cap;
+    hipLaunchKernelGGL((k_ipv4_verify_packed<8, 2>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d,
+                       out, nullptr, nullptr, nullptr, sd, abs_lanes);
+    return launched();
+  }
   const int grid = grid_for(d.n, sh.g);
 #define X(G_, U_)                                                                          \
   if (sh.g == G_ && sh.u == U_) {                                                          \
@@ -1913,6 +1970,17 @@ int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd
 }
 
 int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
+  // packed mixed lengths and dense slots: the flat-run kernel (as verify_plan
+  // picks it for verify), one lane group per datagram otherwise
+  const bool dense_slots = !d.offs && !d.lens && d.stride && d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
+  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
+    uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+    if (blocks > (uint64_t)cap) blocks = cap;
+    hipLaunchKernelGGL((k_ipv4_verify_packed<4, 1>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d,
+                       nullptr, nullptr, nullptr, nullptr, SpanSeeds{}, 0u);
+    return launched();
+  }
   const int grid = grid_for(d.n, sh.g);
 #define X(G_, U_)                                                                  \
   if (sh.g == G_ && sh.u == U_) {                                                  \

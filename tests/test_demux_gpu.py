@@ -57,14 +57,15 @@ def test_demux_verify_golden(demux_golden, kernel):
     assert bad == int(((g["st"] & ~np.uint8(8)) != 0).sum())
 
 
-@pytest.mark.parametrize("shape", [None, (4, 2), (16, 6), (64, 4)])
+@pytest.mark.parametrize("shape", [None, (4, 2), (16, 6), (64, 4), "packed"])
 def test_demux_finalize_golden(demux_golden, shape):
+    """Lane-group shapes and the flat-run finalize (packed hint)."""
     g = demux_golden
-    if shape:
+    if shape and shape != "packed":
         mi.set_shape(shape[0], shape[1], 61)
     try:
         buf = dev(g["fin_in"])
-        mi.ipv4_finalize(batch(buf, g["offs"], g["flen"]))
+        mi.ipv4_finalize(batch(buf, g["offs"], g["flen"], packed=shape == "packed"))
         got = buf.cpu().numpy()
     finally:
         mi.set_shape(0, 0, 0)
@@ -95,7 +96,7 @@ def test_demux_large_mixed(kernel):
     _, h = aligned(d["buf"])
     ORC.ipv4_finalize_batch(h, n, offs=d["offs"], flen=d["flen"], demux=True, nthreads=8)
     buf = dev(d["buf"])
-    mi.ipv4_finalize(batch(buf, d["offs"], d["flen"]))
+    mi.ipv4_finalize(batch(buf, d["offs"], d["flen"], packed=kernel == "packed"))
     assert np.array_equal(buf.cpu().numpy(), h)
     rx = to_rx(h, d, seed=78)
     _, hr = aligned(rx)

@@ -583,3 +583,51 @@ def test_full_size_pareto_and_shards():
         bs = mi.PktBatch(buf, hi - lo, offs=d_offs[lo:hi], lens=d_lens[lo:hi], max_len=int(lens.max()), packed=True)
         rs = mi.ipv4_verify(bs)
         assert np.array_equal(cpu(rs["status"]), st[lo:hi]) and np.array_equal(cpu(rs["l4"]), l4[lo:hi])
+
+
+@pytest.mark.parametrize("hint", [True, False])
+def test_finalize_golden_flat_run(golden, hint):
+    """TX finalize through the flat-run kernel (packed hint) on the reference's
+    golden batch: runts, options, malformed headers, odd starts, UDP / ICMP --
+    byte-identical to the reference's output either way."""
+    g = golden
+    n = len(g["vb_offs"])
+    buf = dev_tensor(g["fin_in"])
+    b = mi.PktBatch(buf, n, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                    lens=dev_tensor(g["vb_flen"].astype(np.int32)), packed=hint)
+    mi.ipv4_finalize(b)
+    assert np.array_equal(cpu(buf), g["fin_out"])
+
+
+@pytest.mark.parametrize("layout", ["packed", "shuffled"])
+def test_span_batch_flat_run(layout):
+    """mi_cksum_span_batch with the packed hint (flat-run span mode): stream and
+    absolute lanes, pseudo-header seeds, empty / odd / long spans (> 65535 B
+    take the per-span fallback) -- equal to the oracle's chains."""
+    rng = np.random.default_rng(9 if layout == "packed" else 10)
+    n = 3000
+    lens = synth.pareto_lengths(n, seed=4)
+    lens[:6] = [0, 1, 2, 3, 65535, 70000]
+    offs = synth.packed_offsets(lens, first_off=3, align=1) + np.arange(n, dtype=np.uint64) % 3
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+        offs, lens = offs[perm], lens[perm]
+    size = int((offs + lens).max()) + 64
+    host = rng.integers(0, 256, size, dtype=np.uint8)
+    buf = dev_tensor(host)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)),
+                    packed=True)
+    src = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    dst = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    proto = rng.integers(0, 256, n).astype(np.uint8)
+    got = cpu(mi.span_batch(b))
+    got_abs = cpu(mi.span_batch(b, mi.MI_SPAN_ABS))
+    got_ps = cpu(mi.span_batch(b, src=dev_tensor(src), dst=dev_tensor(dst), proto=dev_tensor(proto)))
+    _, h = aligned(host)
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        seg = h[o:o + L].tobytes()
+        want = ORC.chain_skip([(seg, o % 64)], L, 0)
+        assert got[i] == want, (i, L, o)
+        assert got_abs[i] == (want if o % 2 == 0 else ((want & 0xFF) << 8) | (want >> 8)), (i, L, o)
+        assert got_ps[i] == ORC.chain_pseudo([(seg, o % 64)], L, 0, int(src[i]), int(dst[i]), int(proto[i])), i
