@@ -91,6 +91,45 @@ def main():
                                                 alg_bytes_per_launch=int(alg)))), flush=True)
         del bufs, outs, plain, demux
         torch.cuda.empty_cache()
+    # scatter-gather: in_cksum_skip over TX socket-buffer chains (a 54 B header
+    # mbuf + 1-2 cluster pieces per 1514 B frame), the L4 part (skip 14 + 20)
+    n = 65536
+    c = synth.build_tx_chains(n, 1500, layout="socket", seed=3)
+    R = max(2, -(-(1 << 30) // c["src"].nbytes))
+    cbs = []
+    for r in range(R):
+        cb = mi.ChainBatch.__new__(mi.ChainBatch)
+        cb.n, cb.max_seg = n, int(c["seg_len"].max())
+        cb.buf = torch.from_numpy(c["src"]).to(dev)
+        cb.seg_off = torch.from_numpy(c["seg_off"].astype(np.int64)).to(dev)
+        cb.seg_len = torch.from_numpy(c["seg_len"].astype(np.int32)).to(dev)
+        cb.pkt_seg = torch.from_numpy(c["pkt_seg"].astype(np.int32)).to(dev)
+        cbs.append(cb)
+    length = torch.from_numpy(c["pkt_len"].astype(np.int32)).to(dev)
+    skip = torch.full((n,), 34, dtype=torch.int32, device=dev)
+    outc = torch.empty(n, dtype=torch.uint16, device=dev)
+    fn = lambda j, s: mi.chain_batch(cbs[j], length, skip, out=outc, stream=s)  # noqa: E731
+    for k in range(20):
+        fn(k % R, streams[k % 2])
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+    e0.record(streams[0])
+    streams[1].wait_event(e0)
+    for k in range(args.steps):
+        fn(k % R, streams[k % 2])
+    for e, s in zip(e1, streams):
+        e.record(s)
+    torch.cuda.synchronize()
+    us = max(e0.elapsed_time(e) for e in e1) * 1e3 / args.steps
+    lsum = int(c["pkt_len"].sum()) - 34 * n
+    alg = lsum + 2 * n
+    print(json.dumps(dict(layout="socket chains 1514 B", op="chain_batch (in_cksum_skip over mbuf chains)",
+                          datagrams=n, segments_per_chain=round(len(c["seg_len"]) / n, 2), us_per_launch=round(us, 2),
+                          GiBps=round(lsum / (us / 1e6) / 2**30, 1),
+                          roofline=dict(bound="hbm", achieved=round(alg / (us / 1e6) / 1e9, 1), peak=PEAK, unit="GB/s",
+                                        frac=round(alg / (us / 1e6) / 1e9 / PEAK, 4), alg_bytes_per_launch=int(alg)))),
+          flush=True)
 
 
 if __name__ == "__main__":
