@@ -133,6 +133,8 @@ int main() {
                 10, a, b, &best);                                                                 \
   report("buffer", U, AUX, grid, med, best);
     RB(4, 0) RB(8, 0) RB(16, 0) RB(4, 2) RB(8, 2) RB(16, 2)
+    // other cache-policy bits (gfx950: bit 0 sc0, bit 1 nt, bit 4 sc1)
+    RB(4, 1) RB(4, 3) RB(4, 16) RB(4, 17) RB(4, 18) RB(4, 19) RB(8, 18) RB(8, 19)
 #define RG(U)                                                                                     \
   med = time_it([&] {                                                                             \
     hipLaunchKernelGGL((rd_global<U>), dim3(grid), dim3(256), 0, 0, (const u32x4 *)buf,            \
