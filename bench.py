@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled (0: enough for >= 1 GiB)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--offs64", action="store_true",
+                    help="pareto: u64 packet offsets instead of u32 (MI_BATCH_OFFS32, 4 B less per datagram)")
     ap.add_argument("--streams", type=int, default=2, help="streams the steps alternate over")
     ap.add_argument("--submit", default="launch", choices=["graph", "launch"],
                     help="launch: K host launches from native code; graph: the same K launches as one cached "
@@ -102,7 +104,8 @@ def main():
         size = int(offs[-1] + lens[-1]) + 64 if n else 64
         workload = f"Pareto 64-9000 B IPv4/TCP RX verify, {total_n} packets split by bytes over {world} GPU(s)"
         scaling = "strong"
-        cfg = dict(workload=workload, packets_total=total_n, packets_this_rank=n, seed="0x9A7E70", alpha=1.16)
+        cfg = dict(workload=workload, packets_total=total_n, packets_this_rank=n, seed="0x9A7E70", alpha=1.16,
+                   offsets="u64" if args.offs64 else "u32")
     else:
         n, L, stride, first = CONFIGS[args.config]
         lens = offs = None
@@ -124,7 +127,7 @@ def main():
         else:
             b = mi.PktBatch(buf, n, offs=torch.from_numpy(offs.astype(np.int64)).to(dev),
                             lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()),
-                            packed=True)
+                            packed=True, offs32=not args.offs64)
         mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r + 104729 * rank)
         mi.ipv4_finalize(b)  # TX path makes every packet valid
         batches.append(b)

@@ -125,6 +125,11 @@ typedef struct mi_pkt_batch {
 /* MI_BATCH_HOST_STAGED: mi_cksum_ipv4_verify_host copies through device
  * staging even when the batch is registered (mapped) host memory. */
 #define MI_BATCH_HOST_STAGED 4u
+/* MI_BATCH_OFFS32: `offs` points to n uint32_t offsets (cast to the field's
+ * type), not uint64_t -- 4 descriptor bytes per packet instead of 8, which a
+ * mixed-length batch of ~280 B datagrams reads beside its payload.  Any batch
+ * (< 4 GiB by the rule above) can use it; results are identical. */
+#define MI_BATCH_OFFS32 8u
 
 /* Lane conventions for mi_cksum_span_batch. */
 #define MI_SPAN_STREAM 0u  /* in_cksum_skip / in_cksum_pseudo_header: lanes

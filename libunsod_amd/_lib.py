@@ -22,6 +22,7 @@ MI_ST_L4_NONE = 8
 MI_BATCH_PACKED = 1
 MI_BATCH_DEMUX = 2
 MI_BATCH_HOST_STAGED = 4
+MI_BATCH_OFFS32 = 8
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2

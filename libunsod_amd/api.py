@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_PACKED, MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_REPEAT_GRAPH, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_OFFS32, MI_BATCH_PACKED,MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_REPEAT_GRAPH, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -106,16 +106,23 @@ class PktBatch:
     to back (MI_BATCH_PACKED hint; correct either way).  ``demux``: verify /
     finalize take each datagram's L4 sum the way ip_input's protocol switch
     hands it on -- TCP / UDP / ICMP / IGMP / CARP, fragments none
-    (MI_BATCH_DEMUX, include/mi_cksum.h).
+    (MI_BATCH_DEMUX, include/mi_cksum.h).  ``offs32``: pass the offsets as
+    u32 (MI_BATCH_OFFS32, 4 descriptor bytes per packet instead of 8).
     """
 
     def __init__(self, buf, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
-                 fixed_len: int = 0, max_len: int = 0, packed: bool = False, demux: bool = False):
+                 fixed_len: int = 0, max_len: int = 0, packed: bool = False, demux: bool = False,
+                 offs32: bool = False):
         torch = _torch()
         if buf.dtype != torch.uint8 or not buf.is_contiguous():
             raise ValueError("buf must be a contiguous uint8 tensor")
+        if buf.numel() >= 1 << 32:
+            raise ValueError("batch buffer must be < 4 GiB")
         self.buf, self.n = buf, int(n)
-        self.offs = None if offs is None else offs.to(torch.int64).contiguous()
+        offs32 = bool(offs32 and offs is not None)
+        # u32 offsets travel as int32 bit patterns (buffers are < 4 GiB)
+        self.offs = None if offs is None else (
+            offs.to(torch.int64).to(torch.int32) if offs32 else offs.to(torch.int64)).contiguous()
         self.lens = None if lens is None else lens.to(torch.int32).contiguous()
         self.stride, self.first_off, self.fixed_len = int(stride), int(first_off), int(fixed_len)
         self.max_len = int(max_len)
@@ -126,7 +133,8 @@ class PktBatch:
                             self.stride, self.first_off,
                             self.lens.data_ptr() if self.lens is not None else None,
                             self.fixed_len, self.n, self.max_len,
-                            (MI_BATCH_PACKED if packed else 0) | (MI_BATCH_DEMUX if demux else 0))
+                            (MI_BATCH_PACKED if packed else 0) | (MI_BATCH_DEMUX if demux else 0)
+                            | (MI_BATCH_OFFS32 if offs32 else 0))
 
     @property
     def c(self) -> PktBatchC:

@@ -145,8 +145,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(d.base), 0, (int)d.bytes,
                                            0x00020000);
 }
+// MI_BATCH_OFFS32: offs holds u32 offsets (half the descriptor bytes); the
+// flag is a kernel argument, so the branch is uniform.
+__device__ __forceinline__ uint64_t desc_off(const Desc &d, uint32_t i) {
+  if (!d.offs) return d.first_off + (uint64_t)i * d.stride;
+  return (d.flags & MI_BATCH_OFFS32) ? (uint64_t)reinterpret_cast<const uint32_t *>(d.offs)[i] : d.offs[i];
+}
 __device__ __forceinline__ uint32_t pkt_off(const Desc &d, uint32_t i) {
-  const uint64_t o = d.offs ? d.offs[i] : d.first_off + (uint64_t)i * d.stride;
+  const uint64_t o = desc_off(d, i);
   return o < kOOB ? (uint32_t)o : kOOB;
 }
 __device__ __forceinline__ uint32_t pkt_len(const Desc &d, uint32_t i) {
@@ -984,7 +990,7 @@ __device__ __forceinline__ void put_be16(uint8_t *p, uint32_t v) {
 __global__ __launch_bounds__(kBlock) void k_synth_hdr(Desc d) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= d.n) return;
-  const uint64_t off = d.offs ? d.offs[i] : d.first_off + (uint64_t)i * d.stride;
+  const uint64_t off = desc_off(d, i);
   const uint32_t len = d.lens ? d.lens[i] : d.fixed_len;
   if (len < 40u || off + 40u > d.bytes) return;
   uint8_t *p = const_cast<uint8_t *>(d.base) + off;
@@ -2442,7 +2448,8 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, ui
   d.first_off = b->first_off;
   d.fixed_len = b->fixed_len;
   if (b->offs) {  // descriptors are small: copy them rather than read them over PCIe per launch
-    HIP_TRY(hipMemcpyAsync(doffs, b->offs, 8 * n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(doffs, b->offs, ((b->flags & MI_BATCH_OFFS32) ? 4 : 8) * n,
+                           hipMemcpyHostToDevice, st));
     d.offs = doffs;
   }
   if (b->lens) {
@@ -2510,7 +2517,11 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
   }();
   const uint8_t *hb = (const uint8_t *)b->base;
   const bool var = b->offs || b->lens;
-  auto off_of = [&](uint32_t i) { return b->offs ? b->offs[i] : b->first_off + (uint64_t)i * b->stride; };
+  const bool o32 = b->flags & MI_BATCH_OFFS32;
+  auto off_of = [&](uint32_t i) -> uint64_t {
+    if (!b->offs) return b->first_off + (uint64_t)i * b->stride;
+    return o32 ? reinterpret_cast<const uint32_t *>(b->offs)[i] : b->offs[i];
+  };
   auto len_of = [&](uint32_t i) { return b->lens ? b->lens[i] : b->fixed_len; };
 
   // Chunks: runs of consecutive packets whose 16-byte envelope fits kChunk
@@ -2583,7 +2594,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
     hipStream_t st = c.hstream[k];
     Desc d{};
     d.len_hi = ~0u;
-    d.flags = b->flags;
+    d.flags = b->flags & ~MI_BATCH_OFFS32;  // staged descriptors are rebuilt as u64
     d.base = c.dstage[k];
     d.bytes = (uint32_t)((end - s0 + 15u) & ~15ull);
     d.n = j - i;

@@ -631,3 +631,55 @@ def test_span_batch_flat_run(layout):
         assert got[i] == want, (i, L, o)
         assert got_abs[i] == (want if o % 2 == 0 else ((want & 0xFF) << 8) | (want >> 8)), (i, L, o)
         assert got_ps[i] == ORC.chain_pseudo([(seg, o % 64)], L, 0, int(src[i]), int(dst[i]), int(proto[i])), i
+
+
+# ------------------------------------------- MI_BATCH_OFFS32 (u32 offsets)
+@pytest.mark.parametrize("layout", ["packed", "shuffled", "gappy"])
+def test_offs32_same_results(golden, layout):
+    """u32 packet offsets (MI_BATCH_OFFS32) give exactly what u64 offsets give:
+    RX verify, RX offload flags, span folds and TX finalize, on a mixed-length
+    batch (packed, shuffled, gappy) and on the reference's golden RX batch."""
+    rng = np.random.default_rng(77)
+    n = 6000
+    lens = synth.pareto_lengths(n, seed=12)
+    offs = synth.packed_offsets(lens, first_off=2)
+    if layout == "gappy":
+        offs = offs + np.arange(n, dtype=np.uint64) * 130
+    b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=13, proto=rng.choice([6, 17], n))
+    _, ref = aligned(b0["buf"])
+    ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32))
+    fin_in = ref.copy()
+    bad = rng.choice(n, 50, replace=False)
+    ref[offs[bad].astype(np.int64) + rng.integers(0, 40, 50)] ^= 0x21
+    perm = rng.permutation(n) if layout == "shuffled" else np.arange(n)
+    o2, l2 = offs[perm], lens[perm]
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(ref, n, offs=o2, flen=l2.astype(np.uint32))
+    buf = dev_tensor(ref)
+    d_lens = dev_tensor(l2.astype(np.int32))
+    b64 = mi.PktBatch(buf, n, offs=dev_tensor(o2.astype(np.int64)), lens=d_lens, packed=True)
+    b32 = mi.PktBatch(buf, n, offs=dev_tensor(o2.astype(np.int64)), lens=d_lens, packed=True, offs32=True)
+    assert b32.offs.dtype == torch.int32 and b32.c.flags & 8
+    r = mi.ipv4_verify(b32, bad_count=True)
+    assert np.array_equal(cpu(r["ip"]), ip_o) and np.array_equal(cpu(r["l4"]), l4_o)
+    assert np.array_equal(cpu(r["status"]), st_o) and int(r["bad"].item()) == int((st_o != 0).sum()) >= 50
+    ro32, ro64 = mi.rx_offload(b32), mi.rx_offload(b64)
+    assert all(torch.equal(ro32[k], ro64[k]) for k in ro64 if torch.is_tensor(ro64[k]))
+    assert torch.equal(mi.span_batch(b32), mi.span_batch(b64))
+    # TX finalize in place, u32 offsets (shuffled order included) == the oracle's finalize
+    _, fsrc = aligned(b0["buf"])
+    fbuf = dev_tensor(fsrc)
+    bf = mi.PktBatch(fbuf, n, offs=dev_tensor(o2.astype(np.int64)), lens=d_lens, packed=True, offs32=True)
+    mi.ipv4_finalize(bf)
+    assert np.array_equal(cpu(fbuf), fin_in)
+    g = golden
+    gn = len(g["vb_offs"])
+    gb = mi.PktBatch(dev_tensor(g["ver_in"]), gn, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                     lens=dev_tensor(g["vb_flen"].astype(np.int32)), packed=True, offs32=True)
+    gr = mi.ipv4_verify(gb)
+    assert np.array_equal(cpu(gr["ip"]), g["ver_ip"]) and np.array_equal(cpu(gr["l4"]), g["ver_l4"])
+    assert np.array_equal(cpu(gr["status"]), g["ver_st"])
+    gbuf = dev_tensor(g["fin_in"])
+    gf = mi.PktBatch(gbuf, gn, offs=dev_tensor(g["vb_offs"].astype(np.int64)),
+                     lens=dev_tensor(g["vb_flen"].astype(np.int32)), packed=True, offs32=True)
+    mi.ipv4_finalize(gf)
+    assert np.array_equal(cpu(gbuf), g["fin_out"])
