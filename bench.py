@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled (0: enough for >= 1 GiB)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the (b1) per-call latency leg")
+    ap.add_argument("--probe-regions", type=int, default=0,
+                    help="diagnostics: time M extra K-step regions first and report their walls (us)")
     ap.add_argument("--offs64", action="store_true",
                     help="pareto: u64 packet offsets instead of u32 (MI_BATCH_OFFS32, 4 B less per datagram)")
     ap.add_argument("--streams", type=int, default=2, help="streams the steps alternate over")
@@ -115,8 +118,14 @@ def main():
         scaling = "weak"
         cfg = dict(workload=workload, packets_per_gpu=n, ip_datagram_len=L, slot_stride=stride, ip_offset=first)
     size = (size + 255) & ~255
-    R = args.rotate or max(1, -(-(1 << 30) // size))  # footprint >= 1 GiB: defeat the 256 MiB MALL
+    # Rotate R distinct batches so that >= 2 GiB of other batches is read between
+    # two reads of the same one: the 256 MiB Infinity Cache then keeps nothing of
+    # a batch (profiles/ceiling_r02.jsonl: at 0.7 GB between reuses 1500 B
+    # verify read ~1.5 % faster than at 2.3 GB).
+    read_per_batch = min(size, L_sum + 16 * n)
+    R = args.rotate or 1 + -(-(2 << 30) // read_per_batch)
     cfg.update(streams=args.streams, rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
+               read_between_reuse_MB=round((R - 1) * read_per_batch / 1e6),
                parallelism=f"dp{world} (independent packet shards, no collective)")
 
     batches, outs = [], []
@@ -141,11 +150,25 @@ def main():
     if int(chk["bad"].item()) != 0:
         raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
 
+    # The K passes are submitted by a prepared handle (mi_cksum_repeat_*: the
+    # descriptors, kernel plans, streams and events are resolved once, as an RX
+    # queue loop re-submitting its rings would), alternating over `nst`
+    # non-blocking streams so a launch's ramp-up overlaps its predecessor's drain.
     nst = max(1, args.streams)
-    tw = time.perf_counter()
     use_graph = args.submit == "graph"
-    if args.warmup:
-        mi.ipv4_verify_repeat(batches, outs, args.warmup, nstreams=nst, timing="none", graph=use_graph)
+    rep = None if use_graph else mi.VerifyRepeat(batches, outs, nstreams=nst)
+
+    def run(k: int, timed: bool = False):
+        if rep is not None:
+            rep.run(k, timed=timed)
+            return rep.span() if timed else None
+        # (the graph path takes at most 16 batches)
+        return mi.ipv4_verify_repeat(batches[:16], outs[:16], k, nstreams=nst,
+                                     timing="region" if timed else "none", graph=True)
+
+    tw = time.perf_counter()
+    if args.warmup:  # timed like the region, so its events are warm too
+        run(args.warmup, timed=True)
     torch.cuda.synchronize()
     # Settle: the first ~0.1 s of back-to-back launches run up to 20 % slower
     # (clock / translation warm-up; profiles/warmup_r01.jsonl: 40 warmup steps ->
@@ -153,30 +176,41 @@ def main():
     # the warmup phase has lasted `--settle` seconds, whatever W is.
     settle_steps = 0
     while time.perf_counter() - tw < args.settle:
-        mi.ipv4_verify_repeat(batches, outs, 500, nstreams=nst, timing="none", graph=use_graph)
+        run(500, timed=True)
         settle_steps += 500
     cfg["settle_steps"] = settle_steps
-    cfg["submit"] = args.submit
+    cfg["submit"] = "graph" if use_graph else "prepared handle, host launches"
     if use_graph:  # instantiate the timed region's graph (K passes) before timing it
-        mi.ipv4_verify_repeat(batches, outs, args.steps, nstreams=nst, timing="none", graph=True)
+        run(args.steps)
+
+    # diagnostics only (--probe-regions M): M extra K-step regions before the
+    # timed one, each bracketed the same way; their walls go to the JSON line
+    probe_walls = []
+    for _ in range(args.probe_regions):
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        run(args.steps, timed=True)
+        torch.cuda.synchronize()
+        probe_walls.append(round((time.perf_counter() - ta) * 1e6, 1))
 
     # ------------------------------------------------------- timed region
-    # K launches issued back to back from native code (libmicksum), alternating
-    # over `nst` non-blocking streams so that a launch's ramp-up overlaps its
-    # predecessor's drain; a hipEvent pair per stream brackets the region.
-    # --submit graph: the same K launches captured once into a hipGraph
-    # (instantiated above, outside the timed region) and replayed.
     K = args.steps
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    span_us = mi.ipv4_verify_repeat(batches, outs, K, nstreams=nst, timing="region", graph=use_graph)
+    if rep is not None:
+        rep.run(K, timed=True)  # launches + hipEvents on the launch streams + wait
+    else:
+        span_us = run(K, timed=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if rep is not None:
+        span_us = rep.span()  # elapsed-time queries after the region
     if dist:
         dist.barrier()
-    elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, float(L_sum) * K, float(n) * K,
+    my_bytes = float(L_sum) * K
+    elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, my_bytes, float(n) * K,
                                                     device=dev if dist and backend == "nccl" else None)
     value = job_bytes / elapsed / GIB
 
@@ -189,22 +223,29 @@ def main():
     gpu_s_per_launch = span_us / K / 1e6
     alg_bytes = float(L_sum) + 5.0 * n
     achieved = alg_bytes / gpu_s_per_launch / 1e9
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    traffic, tsrc = None, None
+    tfile = os.path.join(ROOT, "profiles", "pmc_traffic_r02.json")
+    tkey = args.config + ("_u64" if args.offs64 else "_u32") if args.config == "pareto" else args.config
     if os.path.exists(tfile):
         try:
-            traffic = json.load(open(tfile)).get(args.config, {}).get("bytes_per_launch")
+            ent = json.load(open(tfile)).get(tkey)
+            if ent:
+                traffic = ent["bytes_per_launch"]
+                tsrc = f"profiles/pmc_traffic_r02.json[{tkey}] (rocprofv3 --pmc, separate passes; not this run)"
         except Exception:
             traffic = None
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
                 kernel=mi.verify_plan(batches[0]), alg_bytes_per_launch=int(alg_bytes),
-                avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst)
+                avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst,
+                wall_frac=round(alg_bytes * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))
     # the same kernel alone on one stream, every launch bracketed by events
     # (compare with a single-stream rocprof trace)
-    iso_us, _ = mi.ipv4_verify_repeat(batches, outs, min(K, 100), nstreams=1, timing="pass")
+    iso_us, _ = mi.ipv4_verify_repeat(batches[:16], outs[:16], min(K, 100), nstreams=1, timing="pass")
     roof["isolated_launch_us"] = round(float(np.median(iso_us)), 2)
     roof["isolated_achieved"] = round(alg_bytes / (float(np.median(iso_us)) / 1e6) / 1e9, 1)
+    if rep is not None:
+        rep.close()
 
     result = {
         "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
@@ -213,6 +254,19 @@ def main():
         "data": "synthetic: device-generated IPv4/TCP datagrams (splitmix64 payload), TX-finalized to valid sums",
         "config": cfg, "mpkt_per_s": round(job_pkts / elapsed / 1e6, 2), "roofline": roof,
     }
+    if probe_walls:
+        result["probe_region_walls_us"] = probe_walls
+    if args.config == "64":
+        # every 46 B datagram is one 64 B minimum Ethernet frame (14 B header +
+        # 46 B + 4 B FCS): the frame-equivalent rate SURVEY.md 8(d) asks for
+        result["frame64_equiv_gibs"] = round(job_pkts * 64 / elapsed / GIB, 2)
+    if dist:
+        # per-GPU rates (SURVEY.md 8(e) "Reporting"): timing bookkeeping only
+        mine = torch.tensor([my_bytes, t1 - t0], dtype=torch.float64,
+                            device=dev if backend == "nccl" else None)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        result["per_gpu"] = [round(float(x[0]) / float(x[1]) / GIB, 2) for x in allr]
 
     # -------------------------------------------- CPU baseline + host path
     if world == 1 and rank == 0:
@@ -220,8 +274,11 @@ def main():
         lay = dict(stride=stride, first_off=first, fixed_len=L) if lens is None else dict(offs=offs, lens=lens)
         if args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(host, n, L_sum, lay, args.cpu_seconds)
+            result["cpu_baseline"]["plumbing_64k"] = plumbing_64k()
         if not args.no_host_path:
             result["pcie_inclusive"] = host_path(mi, host, n, L_sum, lay)
+        if not args.no_dropin:
+            result["dropin_latency"] = dropin_latency(mi)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
@@ -277,6 +334,94 @@ def cpu_baseline(host: np.ndarray, n: int, L_sum: int, lay: dict, seconds: float
                                 sample=f"{passes} passes ({dt:.1f} s, {threads} threads, packets split "
                                        f"contiguously)")
     return res
+
+
+def plumbing_64k(seconds: float = 1.0) -> dict:
+    """BASELINE configs[0]: one 64 KiB TCP segment through the reference's
+    in_cksum_skip(m, 65536, 0) on the host CPU (a one-mbuf chain, KAT7
+    pattern; oracle/_ref = the reference's own in_cksum.c), 1 thread, timed in
+    C (batch_driver.c skip_repeat) so no Python sits in the loop."""
+    from oracle.pyoracle import Oracle, available
+    kind = "reference" if available("reference") else "port"
+    o = Oracle(kind)
+    raw = np.zeros(65536 + 128, np.uint8)
+    s = (-raw.ctypes.data) % 64
+    buf = raw[s:s + 65536]
+    buf[:] = np.arange(65536, dtype=np.uint32).astype(np.uint8)
+    assert o.skip_repeat(buf, 65536, 1) == 0x3FC0  # SURVEY KAT7, len 65536
+    iters, dt = 256, 0.0
+    while dt < seconds / 4:
+        t0 = time.perf_counter()
+        o.skip_repeat(buf, 65536, iters)
+        dt = time.perf_counter() - t0
+        iters *= 2
+    iters //= 2
+    t0 = time.perf_counter()
+    n_calls = 0
+    while time.perf_counter() - t0 < seconds:
+        o.skip_repeat(buf, 65536, iters)
+        n_calls += iters
+    dt = time.perf_counter() - t0
+    return dict(value=round(n_calls * 65536 / dt / GIB, 3), unit="GiB/s", us_per_call=round(dt / n_calls * 1e6, 3),
+                cores=1, kind=kind, sample=f"{n_calls} x in_cksum_skip(m, 65536, 0), one L2-resident 64 KiB "
+                                           f"mbuf, {dt:.2f} s")
+
+
+def dropin_latency(mi, calls: int = 400) -> dict:
+    """(b1) drop-in cost per call on this host: libmicksum's in_cksum_hdr /
+    in_cksum_pseudo_header / in_cksum_skip (one GPU launch each, the bytes
+    read over PCIe from pinned staging) against the reference's own functions
+    (oracle/_ref) on the same real mbuf chains.  Median over `calls` calls
+    through ctypes; ``ctypes_floor_us`` is the same loop around in_addword
+    (no checksum work) and is included in every figure."""
+    import ctypes as C
+    from oracle.pyoracle import Oracle, available
+    lib = mi.load()
+    pat = bytes(i & 0xFF for i in range(65536))
+    m64 = mi.MbufChain([pat])
+    ip_hdr = bytes.fromhex("450005dc0000400040060000c0a80101c0a80102")
+    m1500 = mi.MbufChain([ip_hdr + pat[:1480]])
+    hraw = np.zeros(256, np.uint8)
+    hoff = 64 + ((2 - (hraw.ctypes.data + 64)) % 64)  # address == 2 mod 4, as behind a 14 B Ethernet header
+    hraw[hoff:hoff + 20] = np.frombuffer(ip_hdr, np.uint8)
+    haddr = hraw.ctypes.data + hoff
+    src, dst = 0x0101A8C0, 0x0201A8C0  # as loaded (little-endian) from the header
+    cases = {
+        "in_cksum_hdr_20B": ("in_cksum_hdr", (C.c_void_p(haddr),)),
+        "in_cksum_pseudo_header_1480B": ("in_cksum_pseudo_header", (C.c_void_p(m1500.ptr), 1480, 20, src, dst, 6)),
+        "in_cksum_skip_65536B": ("in_cksum_skip", (C.c_void_p(m64.ptr), 65536, 0)),
+    }
+
+    def med(f, args):
+        f(*args)
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            f(*args)
+            ts.append(time.perf_counter() - t0)
+        return round(float(np.median(ts)) * 1e6, 3)
+
+    out = dict(unit="us per call (median)", calls=calls,
+               ctypes_floor_us=med(lib.in_addword, (1, 2)))
+    ref = None
+    if available("reference"):
+        ref = Oracle("reference").lib
+        ref.ref_in_cksum_hdr.restype = C.c_uint
+        ref.ref_in_cksum_hdr.argtypes = [C.c_void_p]
+        ref.ref_in_cksum_skip.restype = C.c_ushort
+        ref.ref_in_cksum_skip.argtypes = [C.c_void_p, C.c_int, C.c_int]
+        ref.ref_in_cksum_pseudo_header.restype = C.c_uint16
+        ref.ref_in_cksum_pseudo_header.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
+                                                   C.c_uint8]
+    for name, (fn, args) in cases.items():
+        g = getattr(lib, fn)
+        row = dict(gpu_dropin_us=med(g, args))
+        if ref is not None:
+            r = getattr(ref, "ref_" + fn)
+            assert int(g(*args)) == int(r(*args)), f"{fn}: drop-in differs from the reference"
+            row["reference_cpu_us"] = med(r, args)
+        out[name] = row
+    return out
 
 
 def _host_threads() -> int:

@@ -284,6 +284,32 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
                                 float *span_us);
 
 /*
+ * The same submission, prepared once (the RX queue loop that re-submits the
+ * same rings): descriptors, kernel plans, nstreams (1..8) non-blocking streams
+ * and events are resolved by mi_cksum_repeat_create, so mi_cksum_repeat_run
+ * costs only its launches and the wait.  Run k of the handle continues the
+ * batch rotation where the previous run stopped.
+ *   flags  MI_TIME_REGION: events bracket the run's passes; *span_us (if not
+ *            NULL) = their GPU span, or read it later with mi_cksum_repeat_span
+ *            (keeps the elapsed-time queries out of a caller's timed region);
+ *          MI_REPEAT_AFTER_DEFAULT: order after the work queued on the legacy
+ *            default stream (otherwise the run starts at once: the caller
+ *            orders earlier producers, e.g. by synchronizing);
+ *          MI_REPEAT_ASYNC: return after submission (mi_cksum_repeat_span
+ *            then waits and reads the span of a timed run).
+ * The handle belongs to the device current at create time; one thread at a
+ * time.  nb <= 1024.  Destroy waits for its streams.
+ */
+#define MI_REPEAT_AFTER_DEFAULT 0x200u
+#define MI_REPEAT_ASYNC         0x400u
+typedef struct mi_repeat mi_repeat;
+int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4,
+                           uint8_t *const *status, uint32_t nstreams, mi_repeat **out);
+int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *span_us);
+int mi_cksum_repeat_span(mi_repeat *r, float *span_us);
+void mi_cksum_repeat_destroy(mi_repeat *r);
+
+/*
  * TX finalize in place (ip_output.c:649-672 + in_delayed_cksum :958-983):
  * for TCP/UDP c = in_cksum_skip(m, ip_len, hl) over the pre-seeded L4 header
  * (UDP: 0 -> 0xffff) stored at hl + (TCP 16 | UDP 6) when inside lens[i]; then

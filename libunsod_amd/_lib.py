@@ -27,6 +27,8 @@ MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2
 MI_REPEAT_GRAPH = 0x100
+MI_REPEAT_AFTER_DEFAULT = 0x200
+MI_REPEAT_ASYNC = 0x400
 MI_CHAIN_SKIP = 0
 MI_CHAIN_PSEUDO = 1
 MI_CSUM_IP_CHECKED = 0x100
@@ -138,6 +140,12 @@ SIGNATURES = {
                                               C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
                                               C.c_uint32, C.c_uint32, C.POINTER(C.c_float),
                                               C.POINTER(C.c_float)]),
+    "mi_cksum_repeat_create": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_uint32,
+                                         C.POINTER(C.c_void_p)]),
+    "mi_cksum_repeat_run": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
+    "mi_cksum_repeat_span": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    "mi_cksum_repeat_destroy": (None, [C.c_void_p]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),

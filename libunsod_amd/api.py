@@ -17,7 +17,9 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_OFFS32, MI_BATCH_PACKED,MI_CHAIN_PSEUDO, MI_CHAIN_SKIP, ChainBatchC, MI_SPAN_ABS, MI_SPAN_STREAM, MI_REPEAT_GRAPH, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, PktBatchC,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_OFFS32, MI_BATCH_PACKED, MI_CHAIN_PSEUDO,
+                   MI_CHAIN_SKIP, MI_REPEAT_AFTER_DEFAULT, MI_REPEAT_ASYNC, MI_REPEAT_GRAPH, MI_SPAN_ABS,
+                   MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, ChainBatchC, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
 
 MSIZE = 256  # param.h:159
@@ -350,6 +352,54 @@ def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str
     return np.frombuffer(us, dtype=np.float32).copy(), float(span.value)
 
 
+class VerifyRepeat:
+    """A prepared back-to-back verify submission (mi_cksum_repeat_*): pass k
+    over batches[k % nb] into outs[k % nb], on the k % nstreams-th of the
+    handle's own non-blocking streams.  Everything is marshalled once here, so
+    ``run`` costs one ctypes call plus the launches and the wait."""
+
+    def __init__(self, batches, outs, nstreams: int = 2):
+        nb = len(batches)
+        self._keep = (batches, outs)
+        arr = (PktBatchC * nb)(*[b.c for b in batches])
+        VP = C.c_void_p * nb
+        ptrs = {k: VP(*[_ptr(o.get(k)) for o in outs]) for k in ("ip", "l4", "status")}
+        h = C.c_void_p()
+        lib = load()
+        check("mi_cksum_repeat_create",
+              lib.mi_cksum_repeat_create(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], nstreams, C.byref(h)))
+        self._h = h
+        self._run = lib.mi_cksum_repeat_run
+        self._span = C.c_float(0.0)
+        self._span_ref = C.byref(self._span)
+
+    def run(self, steps: int, *, timed: bool = False, after_default: bool = False, wait: bool = True) -> None:
+        """Submit ``steps`` passes (and wait for them unless ``wait=False``).
+        ``timed``: hipEvents bracket the passes; read the GPU span with
+        ``span()`` afterwards (outside a caller's timed region)."""
+        flags = ((MI_TIME_REGION if timed else 0) | (MI_REPEAT_AFTER_DEFAULT if after_default else 0)
+                 | (0 if wait else MI_REPEAT_ASYNC))
+        rc = self._run(self._h, steps, flags, None)
+        if rc:
+            check("mi_cksum_repeat_run", rc)
+
+    def span(self) -> float:
+        """Wait for the last timed run and return its GPU span in us."""
+        check("mi_cksum_repeat_span", load().mi_cksum_repeat_span(self._h, self._span_ref))
+        return float(self._span.value)
+
+    def close(self) -> None:
+        if self._h:
+            load().mi_cksum_repeat_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
     """Device-side workload generator (not part of the reference API)."""
     check("mi_cksum_synth_ipv4", load().mi_cksum_synth_ipv4(C.byref(b.c), seed, C.c_void_p(_stream(stream))))
@@ -403,6 +453,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "ipv4_verify_repeat", "host_register", "host_unregister", "set_shape", "init", "device_count", "version",
+    "ipv4_verify_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

@@ -1645,15 +1645,20 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
 }
 
 // Scalar drop-in path: one span in page-locked host memory (read over PCIe).
-__global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
-                                               uint32_t len, uint32_t abs_lanes, int pseudo,
-                                               uint32_t src, uint32_t dst, uint32_t proto,
-                                               uint32_t plen, uint16_t *out) {
+// 8 waves: a pass reads 512 x 4 chunks (32 KiB), so a 64 KiB span costs two
+// PCIe round trips instead of sixteen.  The result goes straight to the
+// caller's pinned slot with a system-scope store, tagged so the host can spin
+// on it (mi__scalar_fold) instead of waiting for the stream.
+constexpr int kScalarThreads = 512;
+__global__ __launch_bounds__(kScalarThreads) void k_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
+                                                          uint32_t len, uint32_t abs_lanes, int pseudo,
+                                                          uint32_t src, uint32_t dst, uint32_t proto,
+                                                          uint32_t plen, uint32_t tag, uint32_t *out) {
   Desc d{};
   d.len_hi = ~0u;
   d.base = base; d.bytes = bytes; d.n = 1; d.first_off = off; d.fixed_len = len;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
-  constexpr int G = 64;
+  constexpr int G = kScalarThreads;
   const int lane = threadIdx.x;
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = len ? (h + len + 15u) >> 4 : 0u;
@@ -1669,12 +1674,19 @@ __global__ __launch_bounds__(64) void k_scalar(const uint8_t *base, uint32_t byt
     }
     acc = fold16(acc);
   }
-  acc = group_sum<G>(acc);
+  __shared__ uint32_t part[kScalarThreads / 64];
+  acc = group_sum<64>(acc);
+  if ((lane & 63) == 0) part[lane >> 6] = acc;
+  __syncthreads();
   if (lane == 0) {
-    uint64_t sum = fold16(acc);
+    uint64_t sum = 0;
+#pragma unroll
+    for (int w = 0; w < kScalarThreads / 64; ++w) sum += part[w];
+    sum = fold16_64(sum);
     if (!abs_lanes && (((uintptr_t)base + off) & 1u)) sum = swap16((uint32_t)sum);
     if (pseudo) sum += (uint64_t)src + dst + (proto << 8) + swap16(plen & 0xffffu);
-    *out = (uint16_t)(~fold16_64(sum) & 0xffffu);
+    const uint32_t res = ~fold16_64(sum) & 0xffffu;
+    __hip_atomic_store(out, (tag << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -1702,8 +1714,11 @@ struct ThreadCtx {
   // scalar (b1) path
   hipStream_t sstream = nullptr;
   uint8_t *stage = nullptr;  // page-locked, device-mapped
+  uint8_t *stage_dev = nullptr;  // its device address (cached: no lookup per call)
   size_t stage_cap = 0;
-  uint16_t *sout = nullptr;  // page-locked result slot
+  uint32_t *sout = nullptr;  // page-locked result slot: (tag << 16) | sum
+  uint32_t *sout_dev = nullptr;
+  uint32_t stag = 0;         // tag of the last scalar call
   // host-batch path
   static constexpr int kRing = 3;
   hipStream_t hstream[kRing] = {};
@@ -1744,6 +1759,53 @@ int check_device(int dev) {
   return 0;
 }
 
+// Free everything a context holds (on its own device; `back` is made current
+// again afterwards).  Errors are ignored: this is cleanup.
+void ctx_release(ThreadCtx &c, int back) {
+  if (hipSetDevice(c.device) != hipSuccess) return;
+  auto stream = [](hipStream_t &s) {
+    if (s) {
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+      s = nullptr;
+    }
+  };
+  auto dfree = [](auto *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+  };
+  auto hfree = [](auto *&p) {
+    if (p) (void)hipHostFree((void *)p);
+    p = nullptr;
+  };
+  stream(c.sstream);
+  hfree(c.stage);
+  hfree(c.sout);
+  for (int k = 0; k < ThreadCtx::kRing; ++k) {
+    stream(c.hstream[k]);
+    dfree(c.dstage[k]);
+    dfree(c.dout[k]);
+    dfree(c.dst8[k]);
+    dfree(c.ddesc[k]);
+    hfree(c.hdesc[k]);
+  }
+  dfree(c.dbad);
+  dfree(c.zbuf);
+  for (int q = 0; q < ThreadCtx::kMaxRep; ++q) {
+    stream(c.rstream[q]);
+    if (c.rjoin[q]) (void)hipEventDestroy(c.rjoin[q]);
+  }
+  for (auto &g : c.rgraph)
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (c.rgate) (void)hipEventDestroy(c.rgate);
+  if (c.rfork) (void)hipEventDestroy(c.rfork);
+  for (uint32_t e = 0; e < c.nev; ++e) (void)hipEventDestroy(c.ev[e]);
+  free(c.ev);
+  c.ev = nullptr;
+  c.nev = 0;
+  (void)hipSetDevice(back);
+}
+
 // Make sure the calling thread has a context on its current HIP device.
 int ensure_ctx() {
   int dev = -1;
@@ -1753,8 +1815,9 @@ int ensure_ctx() {
   int rc = check_device(dev);
   if (rc) return rc;
   if (t_ctx.device != -1) {
-    // thread moved to another device: start a fresh context (old one leaks by design;
-    // its streams belong to the other device)
+    // thread moved to another device: release the old context's streams,
+    // events and buffers on the device they belong to, then start afresh
+    ctx_release(t_ctx, dev);
     t_ctx = ThreadCtx();
   }
   t_ctx.device = dev;
@@ -2303,6 +2366,155 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
   return 0;
 }
 
+}  // extern "C"
+
+// A prepared back-to-back submission (mi_cksum_repeat_*): descriptors, plans,
+// streams and events are resolved once, so a run costs only the launches and
+// the wait -- what an RX queue loop that re-submits the same rings pays.
+struct mi_repeat {
+  int device = -1;
+  uint32_t nb = 0, nstreams = 0;
+  std::vector<Desc> d;
+  std::vector<uint32_t> ml;
+  std::vector<uint16_t *> ip, l4;
+  std::vector<uint8_t *> st;
+  hipStream_t s[ThreadCtx::kMaxRep] = {};
+  hipEvent_t ev0 = nullptr, ev_end[ThreadCtx::kMaxRep] = {};  // timing
+  hipEvent_t ev_done[ThreadCtx::kMaxRep] = {};                // completion only
+  uint32_t next = 0;  // batch the next run starts with (runs continue the rotation)
+};
+
+namespace {
+void repeat_free(mi_repeat *r) {
+  if (!r) return;
+  for (uint32_t q = 0; q < ThreadCtx::kMaxRep; ++q) {
+    if (r->s[q]) (void)hipStreamSynchronize(r->s[q]);
+    if (r->ev_end[q]) (void)hipEventDestroy(r->ev_end[q]);
+    if (r->ev_done[q]) (void)hipEventDestroy(r->ev_done[q]);
+    if (r->s[q]) (void)hipStreamDestroy(r->s[q]);
+  }
+  if (r->ev0) (void)hipEventDestroy(r->ev0);
+  delete r;
+}
+
+// How a synchronous run waits for its last passes (MI_CKSUM_REPEAT_WAIT):
+// "stream" hipStreamSynchronize per stream (default), "event"
+// hipEventSynchronize, "spin" a hipEventQuery loop.  Measured on MI355X
+// (tools/overhead_probe.py, profiles/overhead_r02.jsonl): 20 passes of 1500 B
+// took 311 us of wall clock with "stream" against 343 with "event" or "spin".
+int repeat_wait_mode() {
+  static const int m = [] {
+    const char *e = getenv("MI_CKSUM_REPEAT_WAIT");
+    if (e && !strcmp(e, "event")) return 1;
+    if (e && !strcmp(e, "spin")) return 0;
+    return 2;
+  }();
+  return m;
+}
+}  // namespace
+
+extern "C" {
+
+int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4,
+                           uint8_t *const *status, uint32_t nstreams, mi_repeat **out) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!out) return set_err(-EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!b || !nb) return set_err(-EINVAL, "no batches");
+  if (nb > 1024) return set_err(-EINVAL, "at most 1024 batches");
+  if (nstreams < 1 || nstreams > ThreadCtx::kMaxRep) return set_err(-EINVAL, "nstreams 1..%d", ThreadCtx::kMaxRep);
+  mi_repeat *r = new mi_repeat();
+  r->device = t_ctx.device;
+  r->nb = nb;
+  r->nstreams = nstreams;
+  r->d.resize(nb);
+  r->ml.resize(nb);
+  r->ip.resize(nb);
+  r->l4.resize(nb);
+  r->st.resize(nb);
+  for (uint32_t k = 0; k < nb; ++k) {
+    if ((rc = make_desc(&b[k], &r->d[k]))) {
+      repeat_free(r);
+      return rc;
+    }
+    r->ml[k] = batch_max_len(&b[k]);
+    r->ip[k] = ip ? ip[k] : nullptr;
+    r->l4[k] = l4 ? l4[k] : nullptr;
+    r->st[k] = status ? status[k] : nullptr;
+  }
+  hipError_t e = hipSuccess;
+  for (uint32_t q = 0; q < nstreams && e == hipSuccess; ++q) {
+    e = hipStreamCreateWithFlags(&r->s[q], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&r->ev_end[q]);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev_done[q], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreate(&r->ev0);
+  if (e != hipSuccess) {
+    repeat_free(r);
+    return set_err(-EIO, "repeat_create: %s", hipGetErrorString(e));
+  }
+  *out = r;
+  return 0;
+}
+
+int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *span_us) {
+  if (!r) return set_err(-EINVAL, "handle is NULL");
+  int cur = -1;
+  HIP_TRY(hipGetDevice(&cur));
+  if (cur != r->device) return set_err(-EINVAL, "handle belongs to device %d, thread is on %d", r->device, cur);
+  const bool timed = flags & MI_TIME_REGION;
+  const uint32_t ns = r->nstreams;
+  if (flags & MI_REPEAT_AFTER_DEFAULT) {  // order after the legacy default stream's queued work
+    HIP_TRY(hipEventRecord(r->ev_done[0], nullptr));
+    for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipStreamWaitEvent(r->s[q], r->ev_done[0], 0));
+  }
+  if (timed) {
+    HIP_TRY(hipEventRecord(r->ev0, r->s[0]));
+    for (uint32_t q = 1; q < ns; ++q) HIP_TRY(hipStreamWaitEvent(r->s[q], r->ev0, 0));
+  }
+  int rc = 0;
+  uint32_t j = r->next;
+  for (uint32_t k = 0; k < steps; ++k) {
+    if ((rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]))) return rc;
+    j = j + 1 == r->nb ? 0 : j + 1;
+  }
+  r->next = j;
+  hipEvent_t *fin = timed ? r->ev_end : r->ev_done;
+  for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipEventRecord(fin[q], r->s[q]));
+  if (flags & MI_REPEAT_ASYNC) return 0;
+  const int wm = repeat_wait_mode();
+  for (uint32_t q = 0; q < ns; ++q) {
+    if (wm == 0) {
+      hipError_t e;
+      while ((e = hipEventQuery(fin[q])) == hipErrorNotReady) {
+      }
+      if (e != hipSuccess) return set_err(-EIO, "hipEventQuery: %s", hipGetErrorString(e));
+    } else if (wm == 1) {
+      HIP_TRY(hipEventSynchronize(fin[q]));
+    } else {
+      HIP_TRY(hipStreamSynchronize(r->s[q]));
+    }
+  }
+  if (timed && span_us) return mi_cksum_repeat_span(r, span_us);
+  return 0;
+}
+
+int mi_cksum_repeat_span(mi_repeat *r, float *span_us) {
+  if (!r || !span_us) return set_err(-EINVAL, "NULL argument");
+  float span = 0.f;
+  for (uint32_t q = 0; q < r->nstreams; ++q) {
+    HIP_TRY(hipEventSynchronize(r->ev_end[q]));
+    float end = 0.f;
+    HIP_TRY(hipEventElapsedTime(&end, r->ev0, r->ev_end[q]));
+    if (end > span) span = end;
+  }
+  *span_us = span * 1000.f;
+  return 0;
+}
+
+void mi_cksum_repeat_destroy(mi_repeat *r) { repeat_free(r); }
+
 int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
   int rc = ensure_ctx();
   if (rc) return rc;
@@ -2655,11 +2867,12 @@ uint8_t *mi__scalar_staging(size_t need) {
   if (need < 4096) need = 4096;
   if (c.stage_cap < need) {
     if (c.stage) (void)hipHostFree(c.stage);
-    c.stage = nullptr;
+    c.stage = c.stage_dev = nullptr;
     c.stage_cap = 0;
     size_t cap = 1;
     while (cap < need) cap <<= 1;
     hipError_t e = hipHostMalloc((void **)&c.stage, cap, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c.stage_dev, c.stage, 0);
     if (e != hipSuccess) {
       set_err(-ENOMEM, "hipHostMalloc(%zu): %s", cap, hipGetErrorString(e));
       return nullptr;
@@ -2669,6 +2882,10 @@ uint8_t *mi__scalar_staging(size_t need) {
   return c.stage;
 }
 
+// One launch; the kernel stores (tag << 16) | sum into the pinned slot with a
+// system-scope store and the host spins on the slot (a few us sooner than a
+// stream synchronize).  A call whose slot never turns up within ~1 s falls back
+// to the stream's own wait, so a fault surfaces as an error, never a hang.
 int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32_t src,
                     uint32_t dst, uint8_t proto, uint32_t plen, uint16_t *out) {
   int rc = ensure_ctx();
@@ -2677,17 +2894,30 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   if (!c.stage || off + len > c.stage_cap || c.stage_cap > kMaxBytes)
     return set_err(-EINVAL, "scalar staging overrun");
   if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
-  if (!c.sout) HIP_TRY(hipHostMalloc((void **)&c.sout, 64, hipHostMallocMapped));
-  uint8_t *dstage = nullptr;
-  uint16_t *dout = nullptr;
-  HIP_TRY(hipHostGetDevicePointer((void **)&dstage, c.stage, 0));
-  HIP_TRY(hipHostGetDevicePointer((void **)&dout, c.sout, 0));
-  hipLaunchKernelGGL(k_scalar, dim3(1), dim3(64), 0, c.sstream, (const uint8_t *)dstage,
-                     (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u,
-                     pseudo, src, dst, (uint32_t)proto, plen, dout);
+  if (!c.sout) {
+    HIP_TRY(hipHostMalloc((void **)&c.sout, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
+    memset(c.sout, 0, 64);
+  }
+  c.stag = (c.stag + 1) & 0xffffu;
+  const uint32_t tag = c.stag;
+  hipLaunchKernelGGL(k_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
+                     (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,
+                     (uint32_t)proto, plen, tag, c.sout_dev);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(c.sstream));
-  *out = *(volatile uint16_t *)c.sout;
+  volatile uint32_t *slot = c.sout;
+  uint32_t v = 0;
+  for (uint64_t spin = 0;; ++spin) {
+    v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    if ((v >> 16) == tag) break;
+    if (spin > (1u << 24)) {  // ~1 s: let the runtime report what happened
+      HIP_TRY(hipStreamSynchronize(c.sstream));
+      v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+      if ((v >> 16) != tag) return set_err(-EIO, "scalar fold: no result");
+      break;
+    }
+  }
+  *out = (uint16_t)(v & 0xffffu);
   return 0;
 }
 

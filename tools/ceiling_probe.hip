@@ -1,0 +1,110 @@
+// tools/ceiling_probe.hip -- the read ceiling for the bench's exact pattern
+// (VERDICT r1 item 2): what does a kernel that only READS the bytes the verify
+// kernel reads get, submitted the way bench.py submits verify (back-to-back
+// launches of one BASELINE-sized batch each, alternating over 2 streams, R
+// rotating batches)?  Built as tools/libceiling.so and driven from
+// tools/ceiling.py, which runs the real verify kernel on the same batches in
+// the same process so the two numbers sit side by side.
+//
+//   mode 0  slot envelopes: chunk c of the flat envelope index space (nch
+//           16-byte chunks per datagram, slot * stride + env_off), grid-stride,
+//           U nontemporal buffer loads in flight per lane -- the verify
+//           kernel's bytes without its arithmetic;
+//   mode 1  one contiguous run of the same byte count per batch (no slot
+//           gaps): the best case for the same traffic.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int U>
+__global__ __launch_bounds__(256) void rd_env(const uint8_t *p, uint32_t bytes, uint32_t nslots, uint32_t stride,
+                                             uint32_t env_off, uint32_t nch, uint32_t *sink) {
+  auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), 0, (int)bytes, 0x00020000);
+  const uint32_t nthr = gridDim.x * 256u;
+  const uint32_t total = nslots * nch;
+  uint32_t acc = 0;
+  for (uint32_t c = blockIdx.x * 256u + threadIdx.x; c < total; c += nthr * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      const uint32_t slot = cc / nch, k = cc - slot * nch;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, cc < total ? slot * stride + env_off + 16u * k : 0xFFFFF000u,
+                                                   0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads; practically never stores
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void rd_flat(const uint8_t *p, uint32_t bytes, uint32_t *sink) {
+  auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), 0, (int)bytes, 0x00020000);
+  const uint32_t nthr = gridDim.x * 256u;
+  const uint32_t total = bytes / 16u;
+  uint32_t acc = 0;
+  for (uint32_t c = blockIdx.x * 256u + threadIdx.x; c < total; c += nthr * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, cc < total ? 16u * cc : 0xFFFFF000u, 0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+extern "C" {
+
+// steps launches, launch k over bases[k % nb] on stream k % nstreams (created
+// here, non-blocking); returns the GPU span of all launches in us (events),
+// or a negative value on error.
+float ceil_run(void *const *bases, int nb, uint32_t bytes, uint32_t nslots, uint32_t stride, uint32_t env_off,
+               uint32_t nch, int mode, int unroll, int grid, int steps, int nstreams) {
+  static uint32_t *sink = nullptr;
+  if (!sink && hipMalloc(&sink, 256) != hipSuccess) return -1.f;
+  if (nstreams < 1 || nstreams > 8 || nb < 1) return -2.f;
+  hipStream_t s[8];
+  hipEvent_t e0, e1[8];
+  for (int q = 0; q < nstreams; ++q) {
+    if (hipStreamCreateWithFlags(&s[q], hipStreamNonBlocking) != hipSuccess) return -3.f;
+    if (hipEventCreate(&e1[q]) != hipSuccess) return -3.f;
+  }
+  if (hipEventCreate(&e0) != hipSuccess) return -3.f;
+  hipEventRecord(e0, s[0]);
+  for (int q = 1; q < nstreams; ++q) hipStreamWaitEvent(s[q], e0, 0);
+  const uint32_t flat = nslots * nch * 16u;
+  for (int k = 0; k < steps; ++k) {
+    const uint8_t *p = (const uint8_t *)bases[k % nb];
+    hipStream_t st = s[k % nstreams];
+#define L(U)                                                                                         \
+  if (mode == 0)                                                                                     \
+    hipLaunchKernelGGL((rd_env<U>), dim3(grid), dim3(256), 0, st, p, bytes, nslots, stride, env_off, nch, sink); \
+  else                                                                                               \
+    hipLaunchKernelGGL((rd_flat<U>), dim3(grid), dim3(256), 0, st, p, flat, sink);
+    if (unroll == 2) { L(2) } else if (unroll == 4) { L(4) } else if (unroll == 8) { L(8) } else { L(16) }
+#undef L
+  }
+  for (int q = 0; q < nstreams; ++q) hipEventRecord(e1[q], s[q]);
+  float span = 0.f;
+  for (int q = 0; q < nstreams; ++q) {
+    hipEventSynchronize(e1[q]);
+    float t = 0.f;
+    hipEventElapsedTime(&t, e0, e1[q]);
+    if (t > span) span = t;
+  }
+  if (hipGetLastError() != hipSuccess) span = -4.f / 1000.f;
+  for (int q = 0; q < nstreams; ++q) {
+    hipEventDestroy(e1[q]);
+    hipStreamDestroy(s[q]);
+  }
+  hipEventDestroy(e0);
+  return span * 1000.f;
+}
+
+}  // extern "C"
