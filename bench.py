@@ -55,8 +55,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--no-dropin", action="store_true", help="skip the (b1) per-call latency leg")
-    ap.add_argument("--probe-regions", type=int, default=0,
-                    help="diagnostics: time M extra K-step regions first and report their walls (us)")
+    ap.add_argument("--wait", default="busy", choices=["busy", "auto"],
+                    help="busy: completion waits busy-poll (mi_cksum_set_busy_wait, like the reference's polling "
+                         "dpdk_rx thread); auto: the HIP runtime's default")
+    ap.add_argument("--warm-regions", type=int, default=4,
+                    help="the warmup ends with M untimed K-step regions bracketed like the timed one")
     ap.add_argument("--offs64", action="store_true",
                     help="pareto: u64 packet offsets instead of u32 (MI_BATCH_OFFS32, 4 B less per datagram)")
     ap.add_argument("--streams", type=int, default=2, help="streams the steps alternate over")
@@ -94,6 +97,8 @@ def main():
 
     import libunsod_amd as mi
     from libunsod_amd import shard, synth
+    if args.wait == "busy":
+        mi.set_busy_wait(True)
 
     # ---------------------------------------------------------- workload
     if args.config == "pareto":
@@ -180,18 +185,25 @@ def main():
         settle_steps += 500
     cfg["settle_steps"] = settle_steps
     cfg["submit"] = "graph" if use_graph else "prepared handle, host launches"
+    cfg["wait"] = args.wait
     if use_graph:  # instantiate the timed region's graph (K passes) before timing it
         run(args.steps)
 
-    # diagnostics only (--probe-regions M): M extra K-step regions before the
-    # timed one, each bracketed the same way; their walls go to the JSON line
-    probe_walls = []
-    for _ in range(args.probe_regions):
+    # The warmup ends with M untimed regions of K steps, bracketed exactly like
+    # the timed one: the first region after the settle loop pays ~70-130 us of
+    # host-side wake-up (its GPU span is the same; profiles/bench_regions_r02.jsonl).
+    # Their (wall, span) in us go to the JSON line.
+    warm_walls = []
+    for _ in range(args.warm_regions):
         torch.cuda.synchronize()
         ta = time.perf_counter()
-        run(args.steps, timed=True)
+        if rep is not None:
+            rep.run(args.steps, timed=True)
+        else:
+            run(args.steps, timed=True)
         torch.cuda.synchronize()
-        probe_walls.append(round((time.perf_counter() - ta) * 1e6, 1))
+        w = round((time.perf_counter() - ta) * 1e6, 1)
+        warm_walls.append((w, round(rep.span(), 1)) if rep is not None else w)
 
     # ------------------------------------------------------- timed region
     K = args.steps
@@ -205,8 +217,16 @@ def main():
         span_us = run(K, timed=True)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    trace = None
     if rep is not None:
         span_us = rep.span()  # elapsed-time queries after the region
+        if os.environ.get("MI_CKSUM_REPEAT_TRACE"):
+            import ctypes as C
+            tt = (C.c_double * 8)()
+            mi.load().mi__repeat_trace(rep._h, tt, 8)
+            trace = dict(zip(["entry", "ordered", "first_launch", "last_launch", "markers", "waited"],
+                             [round((tt[k] - t0) * 1e6, 1) for k in range(6)]))
+            trace["t1"] = round((t1 - t0) * 1e6, 1)
     if dist:
         dist.barrier()
     my_bytes = float(L_sum) * K
@@ -254,8 +274,10 @@ def main():
         "data": "synthetic: device-generated IPv4/TCP datagrams (splitmix64 payload), TX-finalized to valid sums",
         "config": cfg, "mpkt_per_s": round(job_pkts / elapsed / 1e6, 2), "roofline": roof,
     }
-    if probe_walls:
-        result["probe_region_walls_us"] = probe_walls
+    if warm_walls:
+        result["warm_region_walls_us"] = warm_walls
+    if trace:
+        result["host_trace_us"] = trace
     if args.config == "64":
         # every 46 B datagram is one 64 B minimum Ethernet frame (14 B header +
         # 46 B + 4 B FCS): the frame-equivalent rate SURVEY.md 8(d) asks for

@@ -310,6 +310,16 @@ int mi_cksum_repeat_span(mi_repeat *r, float *span_us);
 void mi_cksum_repeat_destroy(mi_repeat *r);
 
 /*
+ * Completion waits on the calling thread's current device busy-poll (on != 0:
+ * hipDeviceScheduleSpin) or return to the runtime's default heuristic (0).
+ * A polling RX loop -- like the reference's dpdk_rx kthread spinning on
+ * rte_eth_rx_burst (uinet_if_dpdk.c:900-937) -- wants the wake-up latency of
+ * a spin (~1 us) rather than a blocked wait's (~15-20 us on MI355X,
+ * profiles/bench_regions_r02.jsonl).  Device-wide in the process.
+ */
+int mi_cksum_set_busy_wait(int on);
+
+/*
  * TX finalize in place (ip_output.c:649-672 + in_delayed_cksum :958-983):
  * for TCP/UDP c = in_cksum_skip(m, ip_len, hl) over the pre-seeded L4 header
  * (UDP: 0 -> 0xffff) stored at hl + (TCP 16 | UDP 6) when inside lens[i]; then

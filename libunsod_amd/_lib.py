@@ -146,6 +146,7 @@ SIGNATURES = {
     "mi_cksum_repeat_run": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float)]),
     "mi_cksum_repeat_span": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "mi_cksum_repeat_destroy": (None, [C.c_void_p]),
+    "mi_cksum_set_busy_wait": (C.c_int, [C.c_int]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),

@@ -433,6 +433,11 @@ def host_unregister(buf: np.ndarray) -> None:
     check("mi_cksum_host_unregister", load().mi_cksum_host_unregister(buf.ctypes.data))
 
 
+def set_busy_wait(on: bool = True) -> None:
+    """Busy-poll completion waits on the current device (mi_cksum_set_busy_wait)."""
+    check("mi_cksum_set_busy_wait", load().mi_cksum_set_busy_wait(1 if on else 0))
+
+
 def set_shape(group: int = 0, chunks: int = 0, max_blocks: int = 0) -> None:
     """Force the kernels' lane-group shape / grid cap (0 = automatic); speed only."""
     check("mi_cksum_set_shape", load().mi_cksum_set_shape(group, chunks, max_blocks))
@@ -453,6 +458,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "init", "device_count", "version",
+    "ipv4_verify_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

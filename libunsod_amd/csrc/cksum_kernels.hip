@@ -29,6 +29,7 @@
 // Bit-exactness: the fold is the end-around-carry sum mod 65535 that is zero
 // only for an all-zero input, the same equivalence class REDUCE16 yields, so
 // the association order (lanes, passes, butterfly) cannot change the result.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <errno.h>
@@ -37,6 +38,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <mutex>
 #include <vector>
@@ -1922,13 +1924,31 @@ int launched() {
   return 0;
 }
 
+// Events the NEXT verify launch of this thread carries in its own dispatch
+// (hipExtLaunchKernel start / stop events: no separate marker packets, so the
+// region's first kernel is not queued behind one and completion is the
+// kernel's own signal).  Set by mi_cksum_repeat_run, consumed by VLAUNCH.
+struct LaunchEv {
+  hipEvent_t start = nullptr, stop = nullptr;
+};
+thread_local LaunchEv t_lev;
+#define VLAUNCH(K, GRID, BLOCK, SHM, S, ...)                                                         \
+  do {                                                                                               \
+    if (t_lev.start || t_lev.stop) {                                                                 \
+      const LaunchEv ev_ = t_lev;                                                                    \
+      t_lev = LaunchEv();                                                                            \
+      hipExtLaunchKernelGGL(K, GRID, BLOCK, SHM, S, ev_.start, ev_.stop, 0, __VA_ARGS__);            \
+    } else {                                                                                         \
+      hipLaunchKernelGGL(K, GRID, BLOCK, SHM, S, __VA_ARGS__);                                       \
+    }                                                                                                \
+  } while (0)
+
 int launch_verify_shape(const Desc &d, Shape sh, uint16_t *ip, uint16_t *l4, uint8_t *st,
                         uint32_t *bad, hipStream_t s) {
   const int grid = grid_for(d.n, sh.g);
 #define X(G_, U_)                                                                        \
   if (sh.g == G_ && sh.u == U_) {                                                        \
-    hipLaunchKernelGGL((k_ipv4_verify<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d, ip, l4, \
-                       st, bad);                                                         \
+    VLAUNCH((k_ipv4_verify<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d, ip, l4, st, bad);   \
     return launched();                                                                   \
   }
   FOR_GU(X)
@@ -1989,19 +2009,18 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     if (blocks > (uint64_t)cap) blocks = cap;
     const dim3 grid(blocks ? (unsigned)blocks : 1u);
     if (pl.run_u == 4)
-      hipLaunchKernelGGL((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      VLAUNCH((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     else if (pl.run_u == 16)
-      hipLaunchKernelGGL((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      VLAUNCH((k_ipv4_verify_packed<16>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     else
-      hipLaunchKernelGGL((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      VLAUNCH((k_ipv4_verify_packed<8>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     return launched();
   }
   if (pl.kind == kPlanSlot64) {
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 slots per wave
     if (blocks > (uint64_t)cap) blocks = cap;
-    hipLaunchKernelGGL(k_ipv4_verify_slot64, dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d, ip, l4,
-                       st, bad);
+    VLAUNCH(k_ipv4_verify_slot64, dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d, ip, l4, st, bad);
     return launched();
   }
   if (pl.kind == kPlanShape) return launch_verify_shape(d, pl.shape, ip, l4, st, bad, s);
@@ -2382,6 +2401,11 @@ struct mi_repeat {
   hipEvent_t ev0 = nullptr, ev_end[ThreadCtx::kMaxRep] = {};  // timing
   hipEvent_t ev_done[ThreadCtx::kMaxRep] = {};                // completion only
   uint32_t next = 0;  // batch the next run starts with (runs continue the rotation)
+  // wait mode "flag": every stream writes the run's sequence number into a
+  // pinned host word after its last pass; the host spins on plain memory
+  uint32_t *flag = nullptr, *flag_dev = nullptr;
+  uint32_t seq = 0;
+  double trace[8] = {};  // MI_CKSUM_REPEAT_TRACE: host timestamps of the last run (s)
 };
 
 namespace {
@@ -2394,22 +2418,43 @@ void repeat_free(mi_repeat *r) {
     if (r->s[q]) (void)hipStreamDestroy(r->s[q]);
   }
   if (r->ev0) (void)hipEventDestroy(r->ev0);
+  if (r->flag) (void)hipHostFree(r->flag);
   delete r;
 }
 
 // How a synchronous run waits for its last passes (MI_CKSUM_REPEAT_WAIT):
 // "stream" hipStreamSynchronize per stream (default), "event"
-// hipEventSynchronize, "spin" a hipEventQuery loop.  Measured on MI355X
-// (tools/overhead_probe.py, profiles/overhead_r02.jsonl): 20 passes of 1500 B
-// took 311 us of wall clock with "stream" against 343 with "event" or "spin".
+// hipEventSynchronize, "spin" a hipEventQuery loop, "flag" a spin on pinned
+// host words each stream writes after its last pass (hipStreamWriteValue32).
+// Measured on MI355X (tools/overhead_probe.py, profiles/overhead_*_r02.jsonl):
+// 20 passes of 1500 B took 311 us of wall clock with "stream" against 343
+// with "event" or "spin".
+enum { kWaitSpin, kWaitEvent, kWaitStream, kWaitFlag };
 int repeat_wait_mode() {
   static const int m = [] {
     const char *e = getenv("MI_CKSUM_REPEAT_WAIT");
-    if (e && !strcmp(e, "event")) return 1;
-    if (e && !strcmp(e, "spin")) return 0;
-    return 2;
+    if (e && !strcmp(e, "event")) return (int)kWaitEvent;
+    if (e && !strcmp(e, "spin")) return (int)kWaitSpin;
+    if (e && !strcmp(e, "flag")) return (int)kWaitFlag;
+    return (int)kWaitStream;
   }();
   return m;
+}
+bool repeat_ext_events() {
+  static const bool on = [] {
+    const char *e = getenv("MI_CKSUM_REPEAT_EXT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+bool repeat_trace_on() {
+  static const bool on = getenv("MI_CKSUM_REPEAT_TRACE") != nullptr;
+  return on;
+}
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 }  // namespace
 
@@ -2450,6 +2495,11 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
     if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev_done[q], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreate(&r->ev0);
+  if (e == hipSuccess && repeat_wait_mode() == kWaitFlag) {
+    e = hipHostMalloc((void **)&r->flag, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&r->flag_dev, r->flag, 0);
+    if (e == hipSuccess) memset(r->flag, 0, 64 * sizeof(uint32_t));
+  }
   if (e != hipSuccess) {
     repeat_free(r);
     return set_err(-EIO, "repeat_create: %s", hipGetErrorString(e));
@@ -2460,6 +2510,8 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
 
 int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *span_us) {
   if (!r) return set_err(-EINVAL, "handle is NULL");
+  const bool tr = repeat_trace_on();
+  if (tr) r->trace[0] = now_s();
   int cur = -1;
   HIP_TRY(hipGetDevice(&cur));
   if (cur != r->device) return set_err(-EINVAL, "handle belongs to device %d, thread is on %d", r->device, cur);
@@ -2469,34 +2521,80 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
     HIP_TRY(hipEventRecord(r->ev_done[0], nullptr));
     for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipStreamWaitEvent(r->s[q], r->ev_done[0], 0));
   }
-  if (timed) {
-    HIP_TRY(hipEventRecord(r->ev0, r->s[0]));
-    for (uint32_t q = 1; q < ns; ++q) HIP_TRY(hipStreamWaitEvent(r->s[q], r->ev0, 0));
-  }
+  // Timing events ride on the launches themselves (hipExtLaunchKernel): ev0
+  // starts with the first pass, ev_end[q] stops with stream q's last pass.
+  // A length-class plan (several launches per pass) uses marker events.
+  const bool ext = timed && steps > 0 && repeat_ext_events() &&
+                   verify_plan(r->d[0], r->ml[0]).kind != kPlanClasses;
+  if (timed && !ext) HIP_TRY(hipEventRecord(r->ev0, r->s[0]));
+  if (tr) r->trace[1] = now_s();
   int rc = 0;
   uint32_t j = r->next;
   for (uint32_t k = 0; k < steps; ++k) {
-    if ((rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]))) return rc;
+    if (ext) {
+      t_lev.start = k == 0 ? r->ev0 : nullptr;
+      t_lev.stop = k + ns >= steps ? r->ev_end[k % ns] : nullptr;
+    }
+    rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]);
+    t_lev = LaunchEv();
+    if (rc) return rc;
     j = j + 1 == r->nb ? 0 : j + 1;
+    if (k == 0) {
+      // the other streams start after ev0 (timing); ordered after the first
+      // launch is queued, so the GPU is already busy while the host does it
+      // (with launch-carried events ev0 belongs to pass 0's own dispatch and
+      // the next passes are queued after it; no cross-stream wait)
+      if (timed && !ext)
+        for (uint32_t q = 1; q < ns; ++q) HIP_TRY(hipStreamWaitEvent(r->s[q], r->ev0, 0));
+      if (tr) r->trace[2] = now_s();
+    }
   }
   r->next = j;
+  if (tr) r->trace[3] = now_s();
   hipEvent_t *fin = timed ? r->ev_end : r->ev_done;
-  for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipEventRecord(fin[q], r->s[q]));
-  if (flags & MI_REPEAT_ASYNC) return 0;
   const int wm = repeat_wait_mode();
+  if (!ext && (timed || wm != kWaitFlag || (flags & MI_REPEAT_ASYNC)))
+    for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipEventRecord(fin[q], r->s[q]));
+  if (ext)  // a stream that got no pass this run (steps < ns) still needs its end event
+    for (uint32_t q = steps; q < ns; ++q) HIP_TRY(hipEventRecord(fin[q], r->s[q]));
+  const uint32_t seq = ++r->seq;
+  if (wm == kWaitFlag)
+    for (uint32_t q = 0; q < ns; ++q) HIP_TRY(hipStreamWriteValue32(r->s[q], r->flag_dev + 16 * q, seq, 0));
+  if (tr) r->trace[4] = now_s();
+  if (flags & MI_REPEAT_ASYNC) return 0;
   for (uint32_t q = 0; q < ns; ++q) {
-    if (wm == 0) {
+    if (wm == kWaitSpin) {
       hipError_t e;
       while ((e = hipEventQuery(fin[q])) == hipErrorNotReady) {
       }
       if (e != hipSuccess) return set_err(-EIO, "hipEventQuery: %s", hipGetErrorString(e));
-    } else if (wm == 1) {
+    } else if (wm == kWaitEvent) {
       HIP_TRY(hipEventSynchronize(fin[q]));
+    } else if (wm == kWaitFlag) {
+      const uint32_t *w = r->flag + 16 * q;
+      const double t0 = now_s();
+      uint32_t polls = 0;
+      while (__atomic_load_n(w, __ATOMIC_ACQUIRE) != seq) {
+        if ((++polls & 1023u) == 0 && now_s() - t0 > 2.0) {  // let the runtime report a fault
+          HIP_TRY(hipStreamSynchronize(r->s[q]));
+          if (__atomic_load_n(w, __ATOMIC_ACQUIRE) != seq) return set_err(-EIO, "repeat: completion word not written");
+        }
+      }
     } else {
       HIP_TRY(hipStreamSynchronize(r->s[q]));
     }
   }
+  if (tr) r->trace[5] = now_s();
   if (timed && span_us) return mi_cksum_repeat_span(r, span_us);
+  return 0;
+}
+
+// Diagnostics (not in the public header): host timestamps of the last run
+// with MI_CKSUM_REPEAT_TRACE set -- entry, streams ordered, first launch
+// returned, last launch returned, completion markers queued, wait returned.
+int mi__repeat_trace(mi_repeat *r, double *t, int n) {
+  if (!r || !t) return -EINVAL;
+  for (int k = 0; k < n && k < 8; ++k) t[k] = r->trace[k];
   return 0;
 }
 
@@ -2514,6 +2612,13 @@ int mi_cksum_repeat_span(mi_repeat *r, float *span_us) {
 }
 
 void mi_cksum_repeat_destroy(mi_repeat *r) { repeat_free(r); }
+
+int mi_cksum_set_busy_wait(int on) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  HIP_TRY(hipSetDeviceFlags(on ? hipDeviceScheduleSpin : hipDeviceScheduleAuto));
+  return 0;
+}
 
 int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
   int rc = ensure_ctx();

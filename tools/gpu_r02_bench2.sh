@@ -2,11 +2,8 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
-for i in 1 2 3; do
-  timeout -k 10 180 python -u bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-host-path --no-dropin --probe-regions 8 > gpurun_out/b2_$i.json 2> gpurun_out/b2_$i.err
-  echo "bench $i done"
+rm -f gpurun_out/b5_*.jsonl
+for e in 1 0 1 0; do
+  MI_CKSUM_REPEAT_EXT=$e MI_CKSUM_REPEAT_TRACE=1 timeout -k 10 180 python -u bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-host-path --no-dropin --warm-regions 6 >> gpurun_out/b5_$e.jsonl 2> gpurun_out/b5_$e.err
+  echo "bench $e done"
 done
-for w in spin event; do
-  MI_CKSUM_REPEAT_WAIT=$w timeout -k 10 180 python -u bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 --no-host-path --no-dropin --probe-regions 8 > gpurun_out/b2_$w.json 2> gpurun_out/b2_$w.err
-done
-echo done
