@@ -90,7 +90,8 @@ int mi_cksum_set_shape(int group, int chunks, int max_blocks);
  *   base      16-byte aligned device pointer; [base, base + roundup16(bytes))
  *             must be readable (the kernels load whole 16-byte chunks and rely
  *             on the hardware bounds check of `bytes` for anything beyond).
- *   bytes     buffer size, < 2^32 - 4096.
+ *   bytes     buffer size, <= MI_BATCH_MAX_BYTES (2^32 - 8192: every byte
+ *             offset and the bounds-checked tail stay 32-bit).
  *   Packet i starts at base + (offs ? offs[i] : first_off + i * stride) and is
  *   lens[i] (or fixed_len) bytes long.  offs / lens are device arrays.
  *   max_len   upper bound of lens[] (0 = unknown); sizes the lane groups.
@@ -102,10 +103,14 @@ int mi_cksum_set_shape(int group, int chunks, int max_blocks);
  * Spans outside [0, bytes) read as zero bytes (hardware bounds check), never
  * fault.
  */
+#define MI_BATCH_MAX_BYTES 0xFFFFE000ull
 typedef struct mi_pkt_batch {
 	void           *base;
 	uint64_t        bytes;
-	const uint64_t *offs;
+	union {                         /* device (or, _host calls, host) array */
+		const uint64_t *offs;   /* n u64 offsets */
+		const uint32_t *offs32; /* n u32 offsets, with MI_BATCH_OFFS32 */
+	};
 	uint64_t        stride;
 	uint64_t        first_off;
 	const uint32_t *lens;
@@ -125,10 +130,12 @@ typedef struct mi_pkt_batch {
 /* MI_BATCH_HOST_STAGED: mi_cksum_ipv4_verify_host copies through device
  * staging even when the batch is registered (mapped) host memory. */
 #define MI_BATCH_HOST_STAGED 4u
-/* MI_BATCH_OFFS32: `offs` points to n uint32_t offsets (cast to the field's
- * type), not uint64_t -- 4 descriptor bytes per packet instead of 8, which a
- * mixed-length batch of ~280 B datagrams reads beside its payload.  Any batch
- * (< 4 GiB by the rule above) can use it; results are identical. */
+/* MI_BATCH_OFFS32: the offsets are n uint32_t at `offs32` (same storage as
+ * `offs`) -- 4 descriptor bytes per packet instead of 8, which a mixed-length
+ * batch of ~280 B datagrams reads beside its payload.  Any batch (<=
+ * MI_BATCH_MAX_BYTES) can use it; results are identical to u64 offsets of
+ * the same values.  An offset >= `bytes` is out of range either way
+ * (the datagram reads as zeros and is reported MALFORMED). */
 #define MI_BATCH_OFFS32 8u
 
 /* Lane conventions for mi_cksum_span_batch. */
@@ -308,6 +315,12 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
 int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *span_us);
 int mi_cksum_repeat_span(mi_repeat *r, float *span_us);
 void mi_cksum_repeat_destroy(mi_repeat *r);
+/* What each pass runs: MI_REPEAT_OP_VERIFY (default, mi_cksum_ipv4_verify
+ * into the outputs given at create) or MI_REPEAT_OP_FINALIZE
+ * (mi_cksum_ipv4_finalize in place; outputs unused). */
+#define MI_REPEAT_OP_VERIFY   0u
+#define MI_REPEAT_OP_FINALIZE 1u
+int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op);
 
 /*
  * Completion waits on the calling thread's current device busy-poll (on != 0:
@@ -361,7 +374,7 @@ int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream);
  * Segments (m_data = src + seg_off[k], m_len = seg_len[k], negative = 0) must
  * lie inside [src, src + src_bytes); frame i has segments
  * [pkt_seg[i], pkt_seg[i+1]) and lands at dst + dst_first + i * dst_stride.
- * src, dst 16-byte aligned, both < 4 GiB; l3_off <= 64.  status: n bytes.
+ * src, dst 16-byte aligned, both <= MI_BATCH_MAX_BYTES; l3_off <= 64.  status: n bytes.
  */
 #define MI_CSUM_IP  0x1u
 #define MI_CSUM_TCP 0x2u
@@ -405,6 +418,14 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream);
  */
 int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                               uint8_t *status, uint32_t *bad_count);
+
+/* The RX offload of mi_cksum_rx_offload for a host-resident burst -- the
+ * driver-side hook at the DPDK batch point (uinet_if_dpdk.c:854-879), where
+ * the burst sits in hugepage mbufs: csum_flags / csum_data are host arrays
+ * of n u32 (csum_data may be NULL).  Same transport rules as
+ * mi_cksum_ipv4_verify_host.  Synchronous. */
+int mi_cksum_rx_offload_host(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
+                             uint32_t *bad_count);
 
 /* Page-lock and map / unlock a host range for mi_cksum_ipv4_verify_host
  * (hipHostRegister, mapped + portable). */

@@ -23,12 +23,15 @@ MI_BATCH_PACKED = 1
 MI_BATCH_DEMUX = 2
 MI_BATCH_HOST_STAGED = 4
 MI_BATCH_OFFS32 = 8
+MI_BATCH_MAX_BYTES = 0xFFFFE000  # include/mi_cksum.h
 MI_TIME_NONE = 0
 MI_TIME_REGION = 1
 MI_TIME_PER_PASS = 2
 MI_REPEAT_GRAPH = 0x100
 MI_REPEAT_AFTER_DEFAULT = 0x200
 MI_REPEAT_ASYNC = 0x400
+MI_REPEAT_OP_VERIFY = 0
+MI_REPEAT_OP_FINALIZE = 1
 MI_CHAIN_SKIP = 0
 MI_CHAIN_PSEUDO = 1
 MI_CSUM_IP_CHECKED = 0x100
@@ -147,8 +150,10 @@ SIGNATURES = {
     "mi_cksum_repeat_span": (C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     "mi_cksum_repeat_destroy": (None, [C.c_void_p]),
     "mi_cksum_set_busy_wait": (C.c_int, [C.c_int]),
+    "mi_cksum_repeat_set_op": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
+    "mi_cksum_rx_offload_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),
     "mi_cksum_host_unregister": (C.c_int, [C.c_void_p]),
     "mi_cksum_synth_ipv4": (C.c_int, [C.POINTER(PktBatchC), C.c_uint64, C.c_void_p]),

@@ -17,7 +17,7 @@ from typing import Iterable
 
 import numpy as np
 
-from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_OFFS32, MI_BATCH_PACKED, MI_CHAIN_PSEUDO,
+from ._lib import (MI_BATCH_DEMUX, MI_BATCH_HOST_STAGED, MI_BATCH_OFFS32, MI_BATCH_PACKED, MI_BATCH_MAX_BYTES, MI_CHAIN_PSEUDO,
                    MI_CHAIN_SKIP, MI_REPEAT_AFTER_DEFAULT, MI_REPEAT_ASYNC, MI_REPEAT_GRAPH, MI_SPAN_ABS,
                    MI_SPAN_STREAM, MI_TIME_NONE, MI_TIME_PER_PASS, MI_TIME_REGION, ChainBatchC, PktBatchC,
                    SpanSeedsC, TxBatchC, check, load)
@@ -118,10 +118,13 @@ class PktBatch:
         torch = _torch()
         if buf.dtype != torch.uint8 or not buf.is_contiguous():
             raise ValueError("buf must be a contiguous uint8 tensor")
-        if buf.numel() >= 1 << 32:
-            raise ValueError("batch buffer must be < 4 GiB")
+        if buf.numel() > MI_BATCH_MAX_BYTES:
+            raise ValueError(f"batch buffer of {buf.numel()} B > MI_BATCH_MAX_BYTES ({MI_BATCH_MAX_BYTES})")
         self.buf, self.n = buf, int(n)
         offs32 = bool(offs32 and offs is not None)
+        if offs32 and offs.numel() and int(offs.max().item()) >= 1 << 32:
+            # u32 would wrap such an offset onto valid bytes; u64 reports it MALFORMED
+            raise ValueError("offs32: an offset does not fit in 32 bits")
         # u32 offsets travel as int32 bit patterns (buffers are < 4 GiB)
         self.offs = None if offs is None else (
             offs.to(torch.int64).to(torch.int32) if offs32 else offs.to(torch.int64)).contiguous()
@@ -358,17 +361,21 @@ class VerifyRepeat:
     handle's own non-blocking streams.  Everything is marshalled once here, so
     ``run`` costs one ctypes call plus the launches and the wait."""
 
-    def __init__(self, batches, outs, nstreams: int = 2):
+    def __init__(self, batches, outs=None, nstreams: int = 2, op: str = "verify"):
         nb = len(batches)
         self._keep = (batches, outs)
         arr = (PktBatchC * nb)(*[b.c for b in batches])
         VP = C.c_void_p * nb
+        outs = outs or [{} for _ in batches]
         ptrs = {k: VP(*[_ptr(o.get(k)) for o in outs]) for k in ("ip", "l4", "status")}
         h = C.c_void_p()
         lib = load()
         check("mi_cksum_repeat_create",
               lib.mi_cksum_repeat_create(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], nstreams, C.byref(h)))
         self._h = h
+        if op != "verify":
+            check("mi_cksum_repeat_set_op",
+                  lib.mi_cksum_repeat_set_op(h, {"finalize": 1}[op]))
         self._run = lib.mi_cksum_repeat_run
         self._span = C.c_float(0.0)
         self._span_ref = C.byref(self._span)
@@ -405,24 +412,51 @@ def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
     check("mi_cksum_synth_ipv4", load().mi_cksum_synth_ipv4(C.byref(b.c), seed, C.c_void_p(_stream(stream))))
 
 
-def ipv4_verify_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
-                     fixed_len: int = 0, staged: bool = False, demux: bool = False):
-    """Host-resident batch (mi_cksum_ipv4_verify_host).  Returns numpy
-    (ip, l4, status, bad_count).  A ``buf`` registered with host_register is
-    read in place by the kernel over PCIe (zero-copy) unless ``staged``;
-    otherwise chunked H2D -> verify -> D2H."""
-    offs = None if offs is None else np.ascontiguousarray(offs, np.uint64)
+def _host_batch(buf: np.ndarray, n: int, offs, stride, first_off, lens, fixed_len, staged, demux, offs32):
+    if offs is not None and offs32:
+        o = np.asarray(offs)
+        if o.size and int(o.max()) >= 1 << 32:
+            raise ValueError("offs32: an offset does not fit in 32 bits")
+        offs = np.ascontiguousarray(o, np.uint32)
+    elif offs is not None:
+        offs = np.ascontiguousarray(offs, np.uint64)
     lens = None if lens is None else np.ascontiguousarray(lens, np.uint32)
     hb = PktBatchC(buf.ctypes.data, buf.nbytes, None if offs is None else offs.ctypes.data, stride, first_off,
                    None if lens is None else lens.ctypes.data, fixed_len, n,
                    int(lens.max()) if lens is not None and n else fixed_len,
-                   (MI_BATCH_HOST_STAGED if staged else 0) | (MI_BATCH_DEMUX if demux else 0))
+                   (MI_BATCH_HOST_STAGED if staged else 0) | (MI_BATCH_DEMUX if demux else 0)
+                   | (MI_BATCH_OFFS32 if offs is not None and offs32 else 0))
+    return hb, (offs, lens)
+
+
+def ipv4_verify_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
+                     fixed_len: int = 0, staged: bool = False, demux: bool = False, offs32: bool = False):
+    """Host-resident batch (mi_cksum_ipv4_verify_host).  Returns numpy
+    (ip, l4, status, bad_count).  A ``buf`` registered with host_register is
+    read in place by the kernel over PCIe (zero-copy) unless ``staged``;
+    otherwise chunked H2D -> verify -> D2H.  ``offs32``: pass the offsets as
+    u32 (MI_BATCH_OFFS32)."""
+    hb, keep = _host_batch(buf, n, offs, stride, first_off, lens, fixed_len, staged, demux, offs32)
     ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
     bad = C.c_uint32(0)
     check("mi_cksum_ipv4_verify_host",
           load().mi_cksum_ipv4_verify_host(C.byref(hb), ip.ctypes.data, l4.ctypes.data, st.ctypes.data,
                                            C.addressof(bad)))
+    del keep
     return ip, l4, st, int(bad.value)
+
+
+def rx_offload_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, first_off: int = 0, lens=None,
+                    fixed_len: int = 0, staged: bool = False, demux: bool = False, offs32: bool = False):
+    """RX offload flags for a host-resident burst (mi_cksum_rx_offload_host):
+    numpy (csum_flags u32, csum_data u32, bad_count)."""
+    hb, keep = _host_batch(buf, n, offs, stride, first_off, lens, fixed_len, staged, demux, offs32)
+    fl = np.zeros(n, np.uint32); cd = np.zeros(n, np.uint32)
+    bad = C.c_uint32(0)
+    check("mi_cksum_rx_offload_host",
+          load().mi_cksum_rx_offload_host(C.byref(hb), fl.ctypes.data, cd.ctypes.data, C.addressof(bad)))
+    del keep
+    return fl, cd, int(bad.value)
 
 
 def host_register(buf: np.ndarray) -> None:
@@ -458,6 +492,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
+    "ipv4_verify_host", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

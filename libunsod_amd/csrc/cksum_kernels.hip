@@ -55,7 +55,8 @@ namespace {
 constexpr int kBlock = 256;           // 4 waves
 constexpr int kU = 4;                 // chunks per lane per pass (scalar path)
 constexpr uint32_t kOOB = 0xFFFFF000u;  // offset the bounds check always rejects
-constexpr uint64_t kMaxBytes = 0xFFFFF000ull - 4096;
+constexpr uint64_t kMaxBytes = MI_BATCH_MAX_BYTES;  // == kOOB - 4096: offsets past it stay 32-bit
+static_assert(kMaxBytes == 0xFFFFF000ull - 4096, "kOOB must lie beyond every valid byte");
 
 // ---------------------------------------------------------------- device math
 __device__ __forceinline__ uint32_t fold16(uint32_t x) {
@@ -169,13 +170,13 @@ __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 
 // Issue the U loads of pass p for a packet whose envelope starts at byte c0
 // and has nch chunks; chunks past the envelope get the out-of-range offset.
-template <int G, int U>
+template <int G, int U, int AUX = 2>
 __device__ __forceinline__ void issue_pass(__amdgpu_buffer_rsrc_t r, uint32_t c0, uint32_t nch,
                                            uint32_t p, int lane, u32x4 (&v)[U]) {
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const uint32_t ci = p * (G * U) + u * G + lane;
-    v[u] = ld16(r, ci < nch ? c0 + 16u * ci : kOOB);
+    v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, ci < nch ? c0 + 16u * ci : kOOB, 0, AUX);
   }
 }
 
@@ -313,7 +314,8 @@ template <int G, int U, bool TX>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                           int lane, u32x4 (&v)[U], IpHdr &ih, bool &hdr_ok,
                                           bool &l4_ok, uint32_t &sum_h, uint32_t &sum_l,
-                                          bool demux = false) {
+                                          bool demux = false, u32x4 *keep0 = nullptr) {
+  if (keep0) *keep0 = v[0];  // pass 0, u = 0: chunk `lane` of the envelope (TX whole-block stores)
   const uint32_t c0 = off & ~15u, h = off & 15u;
   const uint32_t nch = (h + flen + 15u) >> 4;
   const uint32_t npass = (nch + G * U - 1) / (G * U);
@@ -355,13 +357,15 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
 // time, with the FIRST pass of the group's next packet issued before the
 // current packet is folded: a group keeps two packets' loads in flight, which
 // is what small datagrams (one pass each) need to cover HBM latency.
-template <int G, int U>
+template <int G, int U, int AUX = 2>
 __device__ __forceinline__ void issue_first(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                             int lane, u32x4 (&v)[U]) {
-  issue_pass<G, U>(r, off & ~15u, flen ? ((off & 15u) + flen + 15u) >> 4 : 0u, 0, lane, v);
+  issue_pass<G, U, AUX>(r, off & ~15u, flen ? ((off & 15u) + flen + 15u) >> 4 : 0u, 0, lane, v);
 }
 
-template <int G, int U, typename Body>
+// AUX0: cache policy of each packet's FIRST pass (2 = nontemporal, as every
+// other read; TX finalize may keep the header lines it writes back into)
+template <int G, int U, typename Body, int AUX0 = 2>
 __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_rsrc_t r, int lane,
                                                 Body body) {
   if (d.lens && (d.len_lo != 0u || d.len_hi != ~0u)) {
@@ -389,7 +393,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
         const uint32_t i = sel[wv * 64u + q];
         const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
         u32x4 v[U];
-        issue_first<G, U>(r, off, flen, lane, v);
+        issue_first<G, U, AUX0>(r, off, flen, lane, v);
         body(i, off, flen, v);
       }
       __builtin_amdgcn_wave_barrier();  // sel[] is rewritten by the next window
@@ -405,14 +409,14 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
     for (; i < d.n; i += stride) {
       const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
       u32x4 v[U];
-      issue_first<G, U>(r, off, flen, lane, v);
+      issue_first<G, U, AUX0>(r, off, flen, lane, v);
       body(i, off, flen, v);
     }
     return;
   }
   uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
   u32x4 v[U];
-  issue_first<G, U>(r, off, flen, lane, v);
+  issue_first<G, U, AUX0>(r, off, flen, lane, v);
   for (;;) {
     const uint32_t in = i + stride;
     const bool more = in < d.n;
@@ -422,7 +426,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
       flenn = pkt_len(d, in);
     }
     u32x4 vn[U];
-    issue_first<G, U>(r, offn, flenn, lane, vn);
+    issue_first<G, U, AUX0>(r, offn, flenn, lane, vn);
     body(i, off, flen, v);
     if (!more) break;
     i = in;
@@ -447,10 +451,11 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
 //    bytes, udp_usrreq.c:406-414); never for fragments (ip_reass sums csum_data of the
 //    pieces, no pseudo header) or other protocols.
 // Malformed headers get no flags: the stack's own length checks drop them.
-__device__ __forceinline__ void rx_offload_store(const Desc &d, __amdgpu_buffer_rsrc_t r, uint32_t i,
-                                                 uint32_t off, const IpHdr &ih, bool hdr_ok,
-                                                 bool l4_ok, uint32_t ip, uint32_t l4) {
-  uint32_t fl = 0, cd = 0;
+__device__ __forceinline__ void rx_offload_flags(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
+                                                 bool hdr_ok, bool l4_ok, uint32_t ip, uint32_t l4, uint32_t &fl,
+                                                 uint32_t &cd) {
+  fl = 0;
+  cd = 0;
   if (hdr_ok) {
     fl = MI_CSUM_IP_CHECKED | (ip ? 0u : MI_CSUM_IP_VALID);
     const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
@@ -470,8 +475,6 @@ __device__ __forceinline__ void rx_offload_store(const Desc &d, __amdgpu_buffer_
       cd = l4 ^ 0xffffu;
     }
   }
-  d.cflags[i] = fl;
-  if (d.cdata) d.cdata[i] = cd;
 }
 
 // ---- small-header callers (MI_BATCH_DEMUX).  Rare
@@ -552,11 +555,20 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
   }
 }
 
-__device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok,
-                                             bool l4_ok, uint32_t sum_h, uint32_t sum_l,
-                                             uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
-                                             uint32_t *bad, const Desc &d,
-                                             __amdgpu_buffer_rsrc_t r, uint32_t off) {
+// One datagram's RX outputs, computed (verify_result) apart from their
+// stores (verify_emit).  On gfx950 vmcnt counts stores with loads, so a store
+// issued before the NEXT datagram's loads makes the wait for those loads wait
+// for the store's acknowledgement too; the kernels therefore emit a
+// datagram's outputs after the next datagram's loads are in flight.
+struct VOut {
+  uint32_t i = ~0u;  // ~0u: nothing pending
+  uint32_t ip = 0, l4 = 0, st = 0, fl = 0, cd = 0;
+};
+__device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok, bool l4_ok,
+                                              uint32_t sum_h, uint32_t sum_l, const Desc &d,
+                                              __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  VOut o;
+  o.i = i;
   uint32_t ip = 0, l4 = 0, st = 0;
   if (!hdr_ok) {
     st = MI_ST_MALFORMED;
@@ -577,11 +589,24 @@ __device__ __forceinline__ void verify_store(uint32_t i, bool odd, const IpHdr &
     }
     st |= (ip ? MI_ST_IP_BAD : 0u) | (l4 ? MI_ST_L4_BAD : 0u);
   }
-  if (ip_out) ip_out[i] = (uint16_t)ip;
-  if (l4_out) l4_out[i] = (uint16_t)l4;
-  if (st_out) st_out[i] = (uint8_t)st;
-  if (bad && (st & ~MI_ST_L4_NONE)) atomicAdd(bad, 1u);
-  if (d.cflags) rx_offload_store(d, r, i, off, ih, hdr_ok, l4_ok, ip, l4);
+  o.ip = ip;
+  o.l4 = l4;
+  o.st = st;
+  if (d.cflags) rx_offload_flags(r, off, ih, hdr_ok, l4_ok, ip, l4, o.fl, o.cd);
+  return o;
+}
+
+__device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                            uint32_t *bad, const Desc &d) {
+  if (o.i == ~0u) return;
+  if (ip_out) ip_out[o.i] = (uint16_t)o.ip;
+  if (l4_out) l4_out[o.i] = (uint16_t)o.l4;
+  if (st_out) st_out[o.i] = (uint8_t)o.st;
+  if (bad && (o.st & ~MI_ST_L4_NONE)) atomicAdd(bad, 1u);
+  if (d.cflags) {
+    d.cflags[o.i] = o.fl;
+    if (d.cdata) d.cdata[o.i] = o.cd;
+  }
 }
 
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
@@ -591,15 +616,16 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
                                                         uint32_t *bad) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
+  VOut pend;  // the previous datagram's outputs, emitted once this one's loads are in flight
   for_each_packet<G, U>(d, r, lane, [&](uint32_t i, uint32_t off, uint32_t flen, u32x4 (&v)[U]) {
+    if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
     IpHdr ih;
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
     ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
-    if (lane == 0)
-      verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
-                   l4_out, st_out, bad, d, r, off);
+    if (lane == 0) pend = verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off);
   });
+  if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
 
 // RX verify of a PACKED batch (MI_BATCH_PACKED: datagrams laid out close
@@ -625,10 +651,18 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 // TX stores of one datagram from its header / L4 sums (ipv4_sums<TX>):
 // in_delayed_cksum (ip_output.c:958-983) or, with MI_BATCH_DEMUX, the
 // small-header senders; then ip_sum = in_cksum(m, hlen) (:667-672).
-__device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen, bool odd,
-                                               const IpHdr &ih, bool hdr_ok, bool do_l4, bool demux,
-                                               uint32_t sum_h, uint32_t sum_l) {
-  if (!(hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen)) return;  // malformed: untouched
+// finalize_plan computes the (at most two) 16-bit fields -- datagram-relative
+// byte position and value in memory order -- and the caller stores them.
+struct TxPatch {
+  uint32_t n = 0;
+  uint32_t at[2] = {0u, 0u};
+  uint32_t val[2] = {0u, 0u};
+};
+__device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen, bool odd,
+                                                 const IpHdr &ih, bool hdr_ok, bool do_l4, bool demux,
+                                                 uint32_t sum_h, uint32_t sum_l) {
+  TxPatch tp;
+  if (!(hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen)) return tp;  // malformed: untouched
   const uint32_t ip_off = ((ih.w[1] >> 8) & 0xff00u) | (ih.w[1] >> 24);
   if (do_l4 && demux && (ip_off & 0x3fffu)) {
     // a fragment: ip_fragment summed the datagram before cutting it
@@ -639,8 +673,8 @@ __device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_
     if (ih.proto == 17u && c == 0u) c = 0xffffu;
     const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
     if (at + 2u <= flen) {
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+      tp.at[tp.n] = at;
+      tp.val[tp.n++] = c;
     }
   } else if (do_l4) {
     // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
@@ -652,16 +686,50 @@ __device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_
       const uint32_t field = odd ? (b0 << 8) + b1 : b0 + (b1 << 8);  // abs lanes, at even
       uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l) - field);
       if (odd) sl = swap16(sl);
-      const uint32_t c = ~sl & 0xffffu;
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + at, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + at + 1u, 0, 0);
+      tp.at[tp.n] = at;
+      tp.val[tp.n++] = ~sl & 0xffffu;
     }
   }
   uint32_t sh = fold16(sum_h);
   if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
-  const uint32_t c = ~sh & 0xffffu;
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c, r, off + 10u, 0, 0);
-  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c >> 8), r, off + 11u, 0, 0);
+  tp.at[tp.n] = 10u;
+  tp.val[tp.n++] = ~sh & 0xffffu;
+  return tp;
+}
+
+// The fields as byte stores (any layout; each store dirties part of a line).
+// MI_TX_STORE_EXP (compile-time, experiments only): 1 = skip the stores,
+// 2 = nontemporal, 3 = sc0 sc1 (write-through).
+#ifndef MI_TX_STORE_EXP
+#define MI_TX_STORE_EXP 0
+#endif
+__device__ __forceinline__ void store_patch_bytes(__amdgpu_buffer_rsrc_t r, uint32_t off, const TxPatch &tp) {
+#if MI_TX_STORE_EXP == 1
+  if (tp.n == 7u) __builtin_amdgcn_raw_buffer_store_b8(0, r, off, 0, 0);  // never: keeps tp live
+  return;
+#endif
+  constexpr int aux = MI_TX_STORE_EXP == 2 ? 2 : MI_TX_STORE_EXP == 3 ? 17 : 0;
+  for (uint32_t k = 0; k < tp.n; ++k) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tp.val[k], r, off + tp.at[k], 0, aux);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(tp.val[k] >> 8), r, off + tp.at[k] + 1u, 0, aux);
+  }
+}
+
+__device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen, bool odd,
+                                               const IpHdr &ih, bool hdr_ok, bool do_l4, bool demux,
+                                               uint32_t sum_h, uint32_t sum_l) {
+  store_patch_bytes(r, off, finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l));
+}
+
+// Byte b (0..15) of chunk v := x.
+__device__ __forceinline__ void chunk_put_byte(u32x4 &v, int b, uint32_t x) {
+  const uint32_t sh = 8u * (b & 3), m = ~(0xffu << sh), y = (x & 0xffu) << sh;
+  switch (b >> 2) {
+    case 0: v.x = (v.x & m) | y; break;
+    case 1: v.y = (v.y & m) | y; break;
+    case 2: v.z = (v.z & m) | y; break;
+    default: v.w = (v.w & m) | y; break;
+  }
 }
 
 // One span's output (k_span's epilogue): the absolute-lane sum S of its bytes,
@@ -754,6 +822,11 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
   // this range is folded
   uint32_t off = p0 + lane < d.n ? pkt_off(d, p0 + lane) : 0u;
   uint32_t flen = p0 + lane < d.n ? pkt_len(d, p0 + lane) : 0u;
+  // this lane's previous datagram's stores, issued once the next range's first
+  // pass is in flight (VOut: vmcnt counts stores with loads)
+  VOut pend;
+  TxPatch ptx;
+  uint32_t ptx_off = 0;
   for (;;) {
     const uint32_t i = p0 + lane;
     const bool act = i < d.n;
@@ -778,6 +851,13 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
       offn = pkt_off(d, pn + lane);
       flenn = pkt_len(d, pn + lane);
     }
+    if constexpr (TX) {
+      if (ptx.n) store_patch_bytes(r, ptx_off, ptx);
+      ptx.n = 0;
+    } else if constexpr (!SPAN) {
+      verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+      pend.i = ~0u;
+    }
     if (!packed) {
       // not packed: one lane per datagram
       if (act && SPAN) {
@@ -793,11 +873,12 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
         uint32_t sum_h, sum_l;
         const bool demux = d.flags & MI_BATCH_DEMUX;
         ipv4_sums<1, 4, TX>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l, demux);
-        if constexpr (TX)
-          finalize_store(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, demux, sum_h, sum_l);
-        else
-          verify_store(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, ip_out,
-                       l4_out, st_out, bad, d, r, off);
+        if constexpr (TX) {
+          ptx = finalize_plan(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, demux, sum_h, sum_l);
+          ptx_off = off;
+        } else {
+          pend = verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off);
+        }
       }
     } else {
       const uint32_t st = act ? off - r0 : 0u, en = act ? end - r0 : 0u;
@@ -882,11 +963,12 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
           for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
             total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
         }
-        if constexpr (TX)
-          finalize_store(r, off, flen, odd, ih, hdr_ok, l4_ok, demux, hdr - field, total - hdr);
-        else
-          verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r,
-                       off);
+        if constexpr (TX) {
+          ptx = finalize_plan(r, off, flen, odd, ih, hdr_ok, l4_ok, demux, hdr - field, total - hdr);
+          ptx_off = off;
+        } else {
+          pend = verify_result(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, d, r, off);
+        }
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -894,6 +976,11 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
     p0 = pn;
     off = offn;
     flen = flenn;
+  }
+  if constexpr (TX) {
+    if (ptx.n) store_patch_bytes(r, ptx_off, ptx);
+  } else if constexpr (!SPAN) {
+    verify_emit(pend, ip_out, l4_out, st_out, bad, d);
   }
 }
 
@@ -913,6 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
   const uint32_t flen = pkt_len(d, 0);
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
   u32x4 *sl = s_slot[wv];
+  VOut pend;  // the previous range's outputs, emitted behind this range's loads
   for (uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u; p0 < d.n; p0 += rstride) {
     const uint32_t base = slot0 + 64u * p0, nslot = min(64u, d.n - p0);
     u32x4 v[4];
@@ -921,6 +1009,8 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
       const uint32_t c = 64u * u + lane;  // chunk of the range: slot c / 4
       v[u] = ld16(r, c < 4u * nslot ? base + 16u * c : kOOB);
     }
+    verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+    pend.i = ~0u;
 #pragma unroll
     for (int u = 0; u < 4; ++u) sl[64u * u + lane] = v[u];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -945,25 +1035,121 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
         total += range_sum(w[j], 16 * j - (int)h, 0, (int)lend);
         hdr += range_sum(w[j], 16 * j - (int)h, 0, (int)hend);
       }
-      verify_store(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, ip_out, l4_out, st_out, bad, d, r, off);
+      pend = verify_result(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, d, r, off);
     }
   }
+  verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
 
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
 // (ip_output.c:667-672).
-template <int G, int U>
+//
+// BLOCKS (host-checked layout, launch_finalize): the 64-byte blocks around a
+// datagram's header hold no byte of any other datagram.  Then the group
+// patches the sum fields into the envelope chunks lanes 0..G-1 still hold
+// from pass 0 and stores every 64-byte block that contains a field WHOLE
+// (its lanes' dwordx4 stores coalesce into one full 64 B write; bytes outside
+// the datagram are rewritten with what was just read).  Byte stores of the
+// 2 + 2 field bytes instead leave partial blocks that the memory side must
+// merge (rocprof: 64 B written per datagram, the launch 45 % slower than
+// verify).  A datagram whose field blocks are not all in pass 0's chunks
+// (envelope starting > 15 B before a block, IP options pushing the L4 field
+// past chunk G) takes the byte stores.
+#ifndef MI_TX_BLOCK
+#define MI_TX_BLOCK 64u
+#endif
+#ifndef MI_TX_FIRST_AUX
+#define MI_TX_FIRST_AUX 2
+#endif
+#if MI_TX_STORE_EXP == 4
+__device__ uint32_t g_tx_sink[1u << 22];
+#endif
+template <int G, int U, bool BLOCKS>
 __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
-  for_each_packet<G, U>(d, r, lane, [&](uint32_t i, uint32_t off, uint32_t flen, u32x4 (&v)[U]) {
+  // The previous datagram's stores, issued once this one's loads are in
+  // flight (see VOut): the byte patch (lane 0) or this lane's block chunk.
+  TxPatch pp;
+  uint32_t poff = 0, pa = kOOB;
+  u32x4 pv = {0, 0, 0, 0};
+  auto flush = [&]() {
+    if (!BLOCKS || pa == kOOB) {
+      if (lane == 0 && pp.n) store_patch_bytes(r, poff, pp);
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b128(pv, r, pa, 0, 0);
+    }
+    pp.n = 0;
+    pa = kOOB;
+  };
+  auto body = [&](uint32_t i, uint32_t off, uint32_t flen, u32x4 (&v)[U]) {
+    flush();
     IpHdr ih;
     bool hdr_ok, do_l4;
     uint32_t sum_h, sum_l;
     const bool demux = d.flags & MI_BATCH_DEMUX;
-    ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux);
-    if (lane == 0) finalize_store(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
-  });
+    const bool odd = ((uintptr_t)d.base + off) & 1u;
+    u32x4 h0;
+#ifdef MI_TX_VERIFY_SUMS
+    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux, BLOCKS ? &h0 : nullptr);
+#else
+    ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux, BLOCKS ? &h0 : nullptr);
+#endif
+    if constexpr (!BLOCKS) {
+#if MI_TX_STORE_EXP == 4
+      if (lane == 0) {
+        const TxPatch tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
+        g_tx_sink[i & ((1u << 22) - 1)] = tp.val[0] ^ (tp.val[1] << 16) ^ tp.n;
+      }
+#else
+      if (lane == 0) {
+        pp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
+        poff = off;
+      }
+#endif
+    } else {
+      TxPatch tp;
+      if (lane == 0) tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
+      const uint32_t n = group_lane<G>(tp.n, 0u);
+      const uint32_t at0 = group_lane<G>(tp.at[0], 0u), at1 = group_lane<G>(tp.at[1], 0u);
+      const uint32_t v0 = group_lane<G>(tp.val[0], 0u), v1 = group_lane<G>(tp.val[1], 0u);
+      const uint32_t c0 = off & ~15u, nch = ((off & 15u) + flen + 15u) >> 4;
+      const uint32_t lim = c0 + 16u * min(nch, (uint32_t)G);  // end of the chunks pass 0 holds in u = 0
+      // the (up to two) 64-byte blocks of each field's two bytes
+      bool ok = flen + (off & (MI_TX_BLOCK - 1u)) <= d.stride;  // (lens[] beyond the max_len hint: byte stores)
+      uint32_t blk[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t at = (k >> 1) ? at1 : at0;
+        blk[k] = (off + at + (k & 1)) & ~(MI_TX_BLOCK - 1u);
+        if ((uint32_t)(k >> 1) < n) ok = ok && blk[k] >= c0 && blk[k] + MI_TX_BLOCK <= lim;
+      }
+      if (!ok) {
+        if (lane == 0) {
+          pp = tp;
+          poff = off;
+        }
+      } else if (n) {
+        const uint32_t a = c0 + 16u * lane;  // this lane's chunk
+        bool dirty = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((uint32_t)(k >> 1) < n) dirty = dirty || (a & ~(MI_TX_BLOCK - 1u)) == blk[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t p = off + ((k >> 1) ? at1 : at0) + (k & 1);
+          const uint32_t b = ((k >> 1) ? v1 : v0) >> (8 * (k & 1));
+          if ((uint32_t)(k >> 1) < n && p - a < 16u) chunk_put_byte(h0, (int)(p - a), b);
+        }
+        if (dirty) {
+          pv = h0;
+          pa = a;
+        }
+      }
+    }
+  };
+  for_each_packet<G, U, decltype(body), MI_TX_FIRST_AUX>(d, r, lane, body);
+  flush();
 }
 
 // ---------------------------------------------------------- workload generator
@@ -1729,6 +1915,7 @@ struct ThreadCtx {
   uint8_t *dst8[kRing] = {};
   uint8_t *ddesc[kRing] = {};  // rebased offs (u64) + lens (u32), device
   uint8_t *hdesc[kRing] = {};  // same, page-locked host
+  uint32_t *dflag[kRing] = {};  // RX offload csum_flags + csum_data, device
   uint32_t *dbad = nullptr;
   size_t dstage_cap = 0, dout_cap = 0;
   // zero-copy host path: device outputs / descriptors (grown on demand)
@@ -1790,6 +1977,7 @@ void ctx_release(ThreadCtx &c, int back) {
     dfree(c.dst8[k]);
     dfree(c.ddesc[k]);
     hfree(c.hdesc[k]);
+    dfree(c.dflag[k]);
   }
   dfree(c.dbad);
   dfree(c.zbuf);
@@ -1890,7 +2078,8 @@ int grid_for(uint32_t n, int G) {
 int make_desc(const mi_pkt_batch *b, Desc *d) {
   if (!b) return set_err(-EINVAL, "batch is NULL");
   if (((uintptr_t)b->base & 15u) != 0) return set_err(-EINVAL, "base %p not 16-byte aligned", b->base);
-  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "batch buffer %llu B >= 4 GiB", (unsigned long long)b->bytes);
+  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "batch buffer %llu B > MI_BATCH_MAX_BYTES (%llu)", (unsigned long long)b->bytes,
+                   (unsigned long long)kMaxBytes);
   if (b->n && !b->base) return set_err(-EINVAL, "base is NULL");
   if (!b->offs && b->n) {
     const uint64_t last = b->first_off + (uint64_t)(b->n - 1) * b->stride;
@@ -2057,7 +2246,27 @@ int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd
   return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
 }
 
-int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
+// k_ipv4_finalize<BLOCKS>'s layout condition: fixed slots (stride a multiple
+// of 64, so every datagram sits at the same phase a = first_off % 64) whose
+// header blocks -- the 64-byte blocks from off - a up to the last one a field
+// can reach (off + 77: hl 60 + TCP sum 16 + 1) -- hold no other datagram's
+// byte: the previous datagram ends by off - a, the next starts after them.
+// MI_CKSUM_TX_BLOCKS=0 turns the whole-block stores off (A/B).
+bool finalize_blocks_ok(const Desc &d, uint32_t max_len) {
+  static const bool allow = [] {
+    const char *e = getenv("MI_CKSUM_TX_BLOCKS");
+    return !(e && e[0] == '0');
+  }();
+  constexpr uint64_t B = MI_TX_BLOCK;
+  if (!allow || d.offs || !d.stride || d.stride % B || !max_len) return false;
+  const uint64_t a = d.first_off % B;
+  const uint64_t hdr_end = ((a + 78u + B - 1) & ~(B - 1));  // block end past the farthest field, from off - a
+  return max_len + a <= d.stride && hdr_end <= d.stride + a;
+}
+
+bool finalize_uses_vlaunch(const Desc &) { return true; }  // every finalize plan is one launch
+
+int launch_finalize(const Desc &d, Shape sh, hipStream_t s, uint32_t max_len) {
   // packed mixed lengths and dense slots: the flat-run kernel (as verify_plan
   // picks it for verify), one lane group per datagram otherwise
   const bool dense_slots = !d.offs && !d.lens && d.stride && d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
@@ -2065,15 +2274,19 @@ int launch_finalize(const Desc &d, Shape sh, hipStream_t s) {
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
     if (blocks > (uint64_t)cap) blocks = cap;
-    hipLaunchKernelGGL((k_ipv4_verify_packed<4, 1>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d,
-                       nullptr, nullptr, nullptr, nullptr, SpanSeeds{}, 0u);
+    VLAUNCH((k_ipv4_verify_packed<4, 1>), dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d, nullptr,
+            nullptr, nullptr, nullptr, SpanSeeds{}, 0u);
     return launched();
   }
   const int grid = grid_for(d.n, sh.g);
-#define X(G_, U_)                                                                  \
-  if (sh.g == G_ && sh.u == U_) {                                                  \
-    hipLaunchKernelGGL((k_ipv4_finalize<G_, U_>), dim3(grid), dim3(kBlock), 0, s, d); \
-    return launched();                                                             \
+  const bool blocks = finalize_blocks_ok(d, max_len) && sh.g >= 4;
+#define X(G_, U_)                                                                          \
+  if (sh.g == G_ && sh.u == U_) {                                                          \
+    if (blocks)                                                                            \
+      VLAUNCH((k_ipv4_finalize<G_, U_, true>), dim3(grid), dim3(kBlock), 0, s, d);         \
+    else                                                                                   \
+      VLAUNCH((k_ipv4_finalize<G_, U_, false>), dim3(grid), dim3(kBlock), 0, s, d);        \
+    return launched();                                                                     \
   }
   FOR_GU(X)
 #undef X
@@ -2172,7 +2385,7 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream) {
   if (!b) return set_err(-EINVAL, "batch is NULL");
   if (!b->n) return 0;
   if (((uintptr_t)b->base & 15u) != 0) return set_err(-EINVAL, "base %p not 16-byte aligned", b->base);
-  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "chain buffer >= 4 GiB");
+  if (b->bytes > kMaxBytes) return set_err(-E2BIG, "chain buffer > MI_BATCH_MAX_BYTES");
   if (!b->base || !b->seg_off || !b->seg_len || !b->pkt_seg || !b->len || !b->skip || !out)
     return set_err(-EINVAL, "NULL array");
   if (b->mode == MI_CHAIN_PSEUDO && (!b->src || !b->dst || !b->proto))
@@ -2401,6 +2614,8 @@ struct mi_repeat {
   hipEvent_t ev0 = nullptr, ev_end[ThreadCtx::kMaxRep] = {};  // timing
   hipEvent_t ev_done[ThreadCtx::kMaxRep] = {};                // completion only
   uint32_t next = 0;  // batch the next run starts with (runs continue the rotation)
+  uint32_t op = MI_REPEAT_OP_VERIFY;
+  std::vector<uint32_t> mlen;  // the finalize layout check's length bound per batch
   // wait mode "flag": every stream writes the run's sequence number into a
   // pinned host word after its last pass; the host spins on plain memory
   uint32_t *flag = nullptr, *flag_dev = nullptr;
@@ -2484,6 +2699,7 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
       return rc;
     }
     r->ml[k] = batch_max_len(&b[k]);
+    r->mlen.push_back(b[k].lens ? b[k].max_len : b[k].fixed_len);
     r->ip[k] = ip ? ip[k] : nullptr;
     r->l4[k] = l4 ? l4[k] : nullptr;
     r->st[k] = status ? status[k] : nullptr;
@@ -2525,7 +2741,8 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
   // starts with the first pass, ev_end[q] stops with stream q's last pass.
   // A length-class plan (several launches per pass) uses marker events.
   const bool ext = timed && steps > 0 && repeat_ext_events() &&
-                   verify_plan(r->d[0], r->ml[0]).kind != kPlanClasses;
+                   (r->op == MI_REPEAT_OP_FINALIZE ? finalize_uses_vlaunch(r->d[0])
+                                                   : verify_plan(r->d[0], r->ml[0]).kind != kPlanClasses);
   if (timed && !ext) HIP_TRY(hipEventRecord(r->ev0, r->s[0]));
   if (tr) r->trace[1] = now_s();
   int rc = 0;
@@ -2535,7 +2752,10 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
       t_lev.start = k == 0 ? r->ev0 : nullptr;
       t_lev.stop = k + ns >= steps ? r->ev_end[k % ns] : nullptr;
     }
-    rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]);
+    if (r->op == MI_REPEAT_OP_FINALIZE)
+      rc = launch_finalize(r->d[j], pick_shape(r->ml[j]), r->s[k % ns], r->mlen[j]);
+    else
+      rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]);
     t_lev = LaunchEv();
     if (rc) return rc;
     j = j + 1 == r->nb ? 0 : j + 1;
@@ -2613,6 +2833,13 @@ int mi_cksum_repeat_span(mi_repeat *r, float *span_us) {
 
 void mi_cksum_repeat_destroy(mi_repeat *r) { repeat_free(r); }
 
+int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op) {
+  if (!r) return set_err(-EINVAL, "handle is NULL");
+  if (op != MI_REPEAT_OP_VERIFY && op != MI_REPEAT_OP_FINALIZE) return set_err(-EINVAL, "op %u", op);
+  r->op = op;
+  return 0;
+}
+
 int mi_cksum_set_busy_wait(int on) {
   int rc = ensure_ctx();
   if (rc) return rc;
@@ -2629,7 +2856,7 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
     return set_err(-EINVAL, "NULL array");
   if (((uintptr_t)b->src & 15u) || ((uintptr_t)b->dst & 15u))
     return set_err(-EINVAL, "src / dst not 16-byte aligned");
-  if (b->src_bytes > kMaxBytes || b->dst_bytes > kMaxBytes) return set_err(-E2BIG, "buffer >= 4 GiB");
+  if (b->src_bytes > kMaxBytes || b->dst_bytes > kMaxBytes) return set_err(-E2BIG, "buffer > MI_BATCH_MAX_BYTES");
   if (b->l3_off > 64) return set_err(-EINVAL, "l3_off %u > 64", b->l3_off);
   const uint64_t last = b->dst_first + (uint64_t)(b->n - 1) * b->dst_stride + b->room;
   if (last > b->dst_bytes)
@@ -2661,7 +2888,8 @@ int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {
   if (rc) return rc;
   if ((rc = make_desc(b, &d))) return rc;
   if (!d.n) return 0;
-  return launch_finalize(d, pick_shape(batch_max_len(b)), (hipStream_t)stream);
+  return launch_finalize(d, pick_shape(batch_max_len(b)), (hipStream_t)stream,
+                         b->lens ? b->max_len : b->fixed_len);
 }
 
 int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
@@ -2733,11 +2961,20 @@ int mi_cksum_host_unregister(void *p) {
 // no DMA engine: only the datagrams' 16-byte envelopes cross the link (slot
 // gaps never do), every read is a wide coalesced load, and the outputs (5 B
 // per datagram) come back with one D2H copy each.
-static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, uint16_t *ip_sum,
-                                 uint16_t *l4_sum, uint8_t *status, uint32_t *bad_count) {
+// Host-side outputs of a host-resident batch (any may be NULL).
+struct HostOut {
+  uint16_t *ip, *l4;
+  uint8_t *st;
+  uint32_t *cflags, *cdata;  // RX offload (mi_cksum_rx_offload_host)
+};
+
+static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, const HostOut &o,
+                                 uint32_t *bad_count) {
+  uint16_t *ip_sum = o.ip, *l4_sum = o.l4;
+  uint8_t *status = o.st;
   ThreadCtx &c = t_ctx;
   const uint64_t n = b->n;
-  const size_t need = 5 * n + 4 + 12 * n + 64;
+  const size_t need = 25 * n + 128;
   if (c.zbuf_cap < need) {
     if (c.zbuf) HIP_TRY(hipFree(c.zbuf));
     c.zbuf = nullptr;
@@ -2755,9 +2992,13 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, ui
   uint16_t *dl4 = dip + n;                         // 2 n
   uint8_t *dst8 = z + 16 * n;                      // n
   uint32_t *dbad = (uint32_t *)(z + ((17 * n + 3) & ~3ull));
+  uint32_t *dcf = (uint32_t *)(z + ((17 * n + 3) & ~3ull) + 16);  // 4 n
+  uint32_t *dcd = dcf + n;                                         // 4 n
   Desc d{};
   d.len_hi = ~0u;
   d.flags = b->flags;
+  d.cflags = o.cflags ? dcf : nullptr;
+  d.cdata = o.cflags && o.cdata ? dcd : nullptr;
   d.base = dbase;
   d.bytes = (uint32_t)((b->bytes + 15u) & ~15ull);
   d.n = b->n;
@@ -2794,6 +3035,8 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, ui
   if (ip_sum) HIP_TRY(hipMemcpyAsync(ip_sum, dip, 2 * n, hipMemcpyDeviceToHost, st));
   if (l4_sum) HIP_TRY(hipMemcpyAsync(l4_sum, dl4, 2 * n, hipMemcpyDeviceToHost, st));
   if (status) HIP_TRY(hipMemcpyAsync(status, dst8, n, hipMemcpyDeviceToHost, st));
+  if (d.cflags) HIP_TRY(hipMemcpyAsync(o.cflags, dcf, 4 * n, hipMemcpyDeviceToHost, st));
+  if (d.cdata) HIP_TRY(hipMemcpyAsync(o.cdata, dcd, 4 * n, hipMemcpyDeviceToHost, st));
   uint32_t bad = 0;
   HIP_TRY(hipMemcpyAsync(&bad, dbad, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -2806,8 +3049,9 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, ui
 // verify -> D2H on a ring of streams, so the copy of chunk k+1 overlaps the
 // kernel of chunk k (PCIe-bound).  MI_CKSUM_HOST_ZC=0 forces
 // the staged path (MI_BATCH_HOST_STAGED per call).
-int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
-                              uint8_t *status, uint32_t *bad_count) {
+static int host_batch(const mi_pkt_batch *b, const HostOut &o, uint32_t *bad_count) {
+  uint16_t *ip_sum = o.ip, *l4_sum = o.l4;
+  uint8_t *status = o.st;
   int rc = ensure_ctx();
   if (rc) return rc;
   if (!b) return set_err(-EINVAL, "batch is NULL");
@@ -2819,12 +3063,12 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
     const char *e = getenv("MI_CKSUM_HOST_ZC");
     return !(e && e[0] == '0');
   }();
-  if (allow_zc && !(b->flags & MI_BATCH_HOST_STAGED) && b->bytes && b->bytes < kMaxBytes &&
+  if (allow_zc && !(b->flags & MI_BATCH_HOST_STAGED) && b->bytes && b->bytes <= kMaxBytes &&
       ((uintptr_t)b->base & 15u) == 0 &&
       host_range_mapped(b->base, b->bytes)) {
     void *dp = nullptr;
     if (hipHostGetDevicePointer(&dp, b->base, 0) == hipSuccess && dp)
-      return verify_host_zero_copy(b, (const uint8_t *)dp, ip_sum, l4_sum, status, bad_count);
+      return verify_host_zero_copy(b, (const uint8_t *)dp, o, bad_count);
     (void)hipGetLastError();  // not registered: staged path
   }
   static const uint64_t kChunk = [] {
@@ -2837,7 +3081,7 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
   const bool o32 = b->flags & MI_BATCH_OFFS32;
   auto off_of = [&](uint32_t i) -> uint64_t {
     if (!b->offs) return b->first_off + (uint64_t)i * b->stride;
-    return o32 ? reinterpret_cast<const uint32_t *>(b->offs)[i] : b->offs[i];
+    return o32 ? b->offs32[i] : b->offs[i];
   };
   auto len_of = [&](uint32_t i) { return b->lens ? b->lens[i] : b->fixed_len; };
 
@@ -2886,6 +3130,8 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
       if (c.dst8[k]) HIP_TRY(hipFree(c.dst8[k]));
       if (c.ddesc[k]) HIP_TRY(hipFree(c.ddesc[k]));
       if (c.hdesc[k]) HIP_TRY(hipHostFree(c.hdesc[k]));
+      if (c.dflag[k]) HIP_TRY(hipFree(c.dflag[k]));
+      HIP_TRY(hipMalloc(&c.dflag[k], 8ull * max_pk));
       HIP_TRY(hipMalloc(&c.dout[k], 4ull * max_pk));
       HIP_TRY(hipMalloc(&c.dst8[k], (size_t)max_pk + 16));
       HIP_TRY(hipMalloc(&c.ddesc[k], 12ull * max_pk));
@@ -2944,12 +3190,17 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
       HIP_TRY(hipMemcpyAsync(c.dstage[k], hb + s0, end - s0, hipMemcpyHostToDevice, st));
     }
     uint16_t *dip = c.dout[k], *dl4 = c.dout[k] + max_pk;
+    uint32_t *dcf = c.dflag[k], *dcd = c.dflag[k] + max_pk;
+    d.cflags = o.cflags ? dcf : nullptr;
+    d.cdata = o.cflags && o.cdata ? dcd : nullptr;
     rc = launch_verify(d, max_len, ip_sum ? dip : nullptr, l4_sum ? dl4 : nullptr,
                        status ? c.dst8[k] : nullptr, c.dbad + k, st);
     if (rc) return rc;
     if (ip_sum) HIP_TRY(hipMemcpyAsync(ip_sum + i, dip, 2ull * d.n, hipMemcpyDeviceToHost, st));
     if (l4_sum) HIP_TRY(hipMemcpyAsync(l4_sum + i, dl4, 2ull * d.n, hipMemcpyDeviceToHost, st));
     if (status) HIP_TRY(hipMemcpyAsync(status + i, c.dst8[k], d.n, hipMemcpyDeviceToHost, st));
+    if (d.cflags) HIP_TRY(hipMemcpyAsync(o.cflags + i, dcf, 4ull * d.n, hipMemcpyDeviceToHost, st));
+    if (d.cdata) HIP_TRY(hipMemcpyAsync(o.cdata + i, dcd, 4ull * d.n, hipMemcpyDeviceToHost, st));
     used[k] = true;
     i = j;
     k = (k + 1) % ThreadCtx::kRing;
@@ -2963,6 +3214,17 @@ int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t 
     *bad_count = t;
   }
   return 0;
+}
+
+int mi_cksum_ipv4_verify_host(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
+                              uint8_t *status, uint32_t *bad_count) {
+  return host_batch(b, HostOut{ip_sum, l4_sum, status, nullptr, nullptr}, bad_count);
+}
+
+int mi_cksum_rx_offload_host(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
+                             uint32_t *bad_count) {
+  if (!csum_flags) return set_err(-EINVAL, "csum_flags is NULL");
+  return host_batch(b, HostOut{nullptr, nullptr, nullptr, csum_flags, csum_data}, bad_count);
 }
 
 // ---------------------------------------------------------- (b1) scalar bridge
