@@ -560,6 +560,15 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
 // issued before the NEXT datagram's loads makes the wait for those loads wait
 // for the store's acknowledgement too; the kernels therefore emit a
 // datagram's outputs after the next datagram's loads are in flight.
+// MI_DEFER=1 emits each datagram's outputs only after the next datagram's
+// loads are issued.  Measured on MI355X (profiles/defer_ab_r02.jsonl, same box,
+// interleaved): verify 1500 B 15.2 vs 14.6 us, Pareto 206 vs 203 us, finalize
+// unchanged -- holding the outputs costs more than the store wait saves, so it
+// is off.
+#ifndef MI_DEFER
+#define MI_DEFER 0
+#endif
+constexpr bool kDefer = MI_DEFER;
 struct VOut {
   uint32_t i = ~0u;  // ~0u: nothing pending
   uint32_t ip = 0, l4 = 0, st = 0, fl = 0, cd = 0;
@@ -623,7 +632,13 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
     ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
-    if (lane == 0) pend = verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off);
+    if (lane == 0) {
+      pend = verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off);
+      if (!kDefer) {
+        verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+        pend.i = ~0u;
+      }
+    }
   });
   if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
@@ -653,10 +668,16 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 // small-header senders; then ip_sum = in_cksum(m, hlen) (:667-672).
 // finalize_plan computes the (at most two) 16-bit fields -- datagram-relative
 // byte position and value in memory order -- and the caller stores them.
-struct TxPatch {
+struct TxPatch {  // plain fields: an indexed array would be promoted to LDS / scratch
   uint32_t n = 0;
-  uint32_t at[2] = {0u, 0u};
-  uint32_t val[2] = {0u, 0u};
+  uint32_t at0 = 0, val0 = 0, at1 = 0, val1 = 0;
+  __device__ __forceinline__ void add(uint32_t at, uint32_t v) {  // selects, not a branch on n
+    at0 = n == 0 ? at : at0;
+    val0 = n == 0 ? v : val0;
+    at1 = n == 1 ? at : at1;
+    val1 = n == 1 ? v : val1;
+    ++n;
+  }
 };
 __device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen, bool odd,
                                                  const IpHdr &ih, bool hdr_ok, bool do_l4, bool demux,
@@ -672,10 +693,7 @@ __device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint3
     uint32_t c = ~sl & 0xffffu;
     if (ih.proto == 17u && c == 0u) c = 0xffffu;
     const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
-    if (at + 2u <= flen) {
-      tp.at[tp.n] = at;
-      tp.val[tp.n++] = c;
-    }
+    if (at + 2u <= flen) tp.add(at, c);
   } else if (do_l4) {
     // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
     const bool carp = ih.proto == 112u;
@@ -686,14 +704,12 @@ __device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint3
       const uint32_t field = odd ? (b0 << 8) + b1 : b0 + (b1 << 8);  // abs lanes, at even
       uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l) - field);
       if (odd) sl = swap16(sl);
-      tp.at[tp.n] = at;
-      tp.val[tp.n++] = ~sl & 0xffffu;
+      tp.add(at, ~sl & 0xffffu);
     }
   }
   uint32_t sh = fold16(sum_h);
   if (odd) sh = swap16(sh);  // in_cksum(m, hlen): stream lanes
-  tp.at[tp.n] = 10u;
-  tp.val[tp.n++] = ~sh & 0xffffu;
+  tp.add(10u, ~sh & 0xffffu);
   return tp;
 }
 
@@ -709,9 +725,13 @@ __device__ __forceinline__ void store_patch_bytes(__amdgpu_buffer_rsrc_t r, uint
   return;
 #endif
   constexpr int aux = MI_TX_STORE_EXP == 2 ? 2 : MI_TX_STORE_EXP == 3 ? 17 : 0;
-  for (uint32_t k = 0; k < tp.n; ++k) {
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tp.val[k], r, off + tp.at[k], 0, aux);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(tp.val[k] >> 8), r, off + tp.at[k] + 1u, 0, aux);
+  if (tp.n > 0) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tp.val0, r, off + tp.at0, 0, aux);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(tp.val0 >> 8), r, off + tp.at0 + 1u, 0, aux);
+  }
+  if (tp.n > 1) {
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tp.val1, r, off + tp.at1, 0, aux);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(tp.val1 >> 8), r, off + tp.at1 + 1u, 0, aux);
   }
 }
 
@@ -724,12 +744,11 @@ __device__ __forceinline__ void finalize_store(__amdgpu_buffer_rsrc_t r, uint32_
 // Byte b (0..15) of chunk v := x.
 __device__ __forceinline__ void chunk_put_byte(u32x4 &v, int b, uint32_t x) {
   const uint32_t sh = 8u * (b & 3), m = ~(0xffu << sh), y = (x & 0xffu) << sh;
-  switch (b >> 2) {
-    case 0: v.x = (v.x & m) | y; break;
-    case 1: v.y = (v.y & m) | y; break;
-    case 2: v.z = (v.z & m) | y; break;
-    default: v.w = (v.w & m) | y; break;
-  }
+  const int q = b >> 2;  // selects, no indexing (an indexed vector would go to scratch)
+  v.x = q == 0 ? (v.x & m) | y : v.x;
+  v.y = q == 1 ? (v.y & m) | y : v.y;
+  v.z = q == 2 ? (v.z & m) | y : v.z;
+  v.w = q == 3 ? (v.w & m) | y : v.w;
 }
 
 // One span's output (k_span's epilogue): the absolute-lane sum S of its bytes,
@@ -876,8 +895,16 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
         if constexpr (TX) {
           ptx = finalize_plan(r, off, flen, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, demux, sum_h, sum_l);
           ptx_off = off;
+          if (!kDefer) {
+            store_patch_bytes(r, ptx_off, ptx);
+            ptx.n = 0;
+          }
         } else {
           pend = verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off);
+          if (!kDefer) {
+            verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+            pend.i = ~0u;
+          }
         }
       }
     } else {
@@ -966,8 +993,16 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
         if constexpr (TX) {
           ptx = finalize_plan(r, off, flen, odd, ih, hdr_ok, l4_ok, demux, hdr - field, total - hdr);
           ptx_off = off;
+          if (!kDefer) {
+            store_patch_bytes(r, ptx_off, ptx);
+            ptx.n = 0;
+          }
         } else {
           pend = verify_result(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, d, r, off);
+          if (!kDefer) {
+            verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+            pend.i = ~0u;
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -1036,6 +1071,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
         hdr += range_sum(w[j], 16 * j - (int)h, 0, (int)hend);
       }
       pend = verify_result(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, d, r, off);
+      if (!kDefer) {
+        verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+        pend.i = ~0u;
+      }
     }
   }
   verify_emit(pend, ip_out, l4_out, st_out, bad, d);
@@ -1099,7 +1138,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
 #if MI_TX_STORE_EXP == 4
       if (lane == 0) {
         const TxPatch tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
-        g_tx_sink[i & ((1u << 22) - 1)] = tp.val[0] ^ (tp.val[1] << 16) ^ tp.n;
+        g_tx_sink[i & ((1u << 22) - 1)] = tp.val0 ^ (tp.val1 << 16) ^ tp.n;
       }
 #else
       if (lane == 0) {
@@ -1111,19 +1150,17 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
       TxPatch tp;
       if (lane == 0) tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
       const uint32_t n = group_lane<G>(tp.n, 0u);
-      const uint32_t at0 = group_lane<G>(tp.at[0], 0u), at1 = group_lane<G>(tp.at[1], 0u);
-      const uint32_t v0 = group_lane<G>(tp.val[0], 0u), v1 = group_lane<G>(tp.val[1], 0u);
+      const uint32_t at0 = group_lane<G>(tp.at0, 0u), at1 = group_lane<G>(tp.at1, 0u);
+      const uint32_t v0 = group_lane<G>(tp.val0, 0u), v1 = group_lane<G>(tp.val1, 0u);
       const uint32_t c0 = off & ~15u, nch = ((off & 15u) + flen + 15u) >> 4;
       const uint32_t lim = c0 + 16u * min(nch, (uint32_t)G);  // end of the chunks pass 0 holds in u = 0
       // the (up to two) 64-byte blocks of each field's two bytes
       bool ok = flen + (off & (MI_TX_BLOCK - 1u)) <= d.stride;  // (lens[] beyond the max_len hint: byte stores)
-      uint32_t blk[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t at = (k >> 1) ? at1 : at0;
-        blk[k] = (off + at + (k & 1)) & ~(MI_TX_BLOCK - 1u);
-        if ((uint32_t)(k >> 1) < n) ok = ok && blk[k] >= c0 && blk[k] + MI_TX_BLOCK <= lim;
-      }
+      // the blocks of each field's first and second byte
+      const uint32_t b0 = (off + at0) & ~(MI_TX_BLOCK - 1u), b1 = (off + at0 + 1u) & ~(MI_TX_BLOCK - 1u);
+      const uint32_t b2 = (off + at1) & ~(MI_TX_BLOCK - 1u), b3 = (off + at1 + 1u) & ~(MI_TX_BLOCK - 1u);
+      auto fits = [&](uint32_t b) { return b >= c0 && b + MI_TX_BLOCK <= lim; };
+      ok = ok && (n < 1 || (fits(b0) && fits(b1))) && (n < 2 || (fits(b2) && fits(b3)));
       if (!ok) {
         if (lane == 0) {
           pp = tp;
@@ -1131,22 +1168,20 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
         }
       } else if (n) {
         const uint32_t a = c0 + 16u * lane;  // this lane's chunk
-        bool dirty = false;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if ((uint32_t)(k >> 1) < n) dirty = dirty || (a & ~(MI_TX_BLOCK - 1u)) == blk[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t p = off + ((k >> 1) ? at1 : at0) + (k & 1);
-          const uint32_t b = ((k >> 1) ? v1 : v0) >> (8 * (k & 1));
-          if ((uint32_t)(k >> 1) < n && p - a < 16u) chunk_put_byte(h0, (int)(p - a), b);
-        }
+        const uint32_t ab = a & ~(MI_TX_BLOCK - 1u);
+        const bool dirty = (n >= 1 && (ab == b0 || ab == b1)) || (n >= 2 && (ab == b2 || ab == b3));
+        const uint32_t p0 = off + at0, p1 = off + at1;
+        if (n >= 1 && p0 - a < 16u) chunk_put_byte(h0, (int)(p0 - a), v0);
+        if (n >= 1 && p0 + 1u - a < 16u) chunk_put_byte(h0, (int)(p0 + 1u - a), v0 >> 8);
+        if (n >= 2 && p1 - a < 16u) chunk_put_byte(h0, (int)(p1 - a), v1);
+        if (n >= 2 && p1 + 1u - a < 16u) chunk_put_byte(h0, (int)(p1 + 1u - a), v1 >> 8);
         if (dirty) {
           pv = h0;
           pa = a;
         }
       }
     }
+    if (!kDefer) flush();
   };
   for_each_packet<G, U, decltype(body), MI_TX_FIRST_AUX>(d, r, lane, body);
   flush();
@@ -2251,12 +2286,15 @@ int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd
 // header blocks -- the 64-byte blocks from off - a up to the last one a field
 // can reach (off + 77: hl 60 + TCP sum 16 + 1) -- hold no other datagram's
 // byte: the previous datagram ends by off - a, the next starts after them.
-// MI_CKSUM_TX_BLOCKS=0 turns the whole-block stores off (A/B).
+// Off by default, MI_CKSUM_TX_BLOCKS=1 turns the whole-block stores on: on
+// MI355X they measured no faster than the byte stores (1500 B 36.4 vs 34.5 us,
+// 9000 B 100.7 vs 97.9 us, profiles/finalize_r02.jsonl), and a bare read +
+// 64 B-block store probe costs the same as read + 4 B store
+// (profiles/ceiling_writes_r02.jsonl): the price is the scattered write, not
+// its width.
 bool finalize_blocks_ok(const Desc &d, uint32_t max_len) {
-  static const bool allow = [] {
-    const char *e = getenv("MI_CKSUM_TX_BLOCKS");
-    return !(e && e[0] == '0');
-  }();
+  const char *e = getenv("MI_CKSUM_TX_BLOCKS");  // per launch, so tests can switch it
+  const bool allow = e && e[0] == '1';
   constexpr uint64_t B = MI_TX_BLOCK;
   if (!allow || d.offs || !d.stride || d.stride % B || !max_len) return false;
   const uint64_t a = d.first_off % B;

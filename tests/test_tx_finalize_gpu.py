@@ -6,9 +6,12 @@ whose blocks run past the envelope, per-packet lens under a max_len hint and
 lens beyond it, MI_BATCH_DEMUX small-header senders.  The whole buffer must
 equal the oracle's finalize byte for byte -- which also proves that the
 rewritten bytes around each datagram are unchanged."""
+import os
+
 import numpy as np
 import pytest
 import torch
+
 
 import libunsod_amd as mi
 from conftest import aligned
@@ -17,6 +20,13 @@ from oracle.pyoracle import Oracle
 
 pytestmark = pytest.mark.gpu
 ORC = Oracle("port")
+
+
+@pytest.fixture(autouse=True, params=["blocks", "bytes"])
+def tx_store_mode(request, monkeypatch):
+    """Both store schemes (the library reads MI_CKSUM_TX_BLOCKS per launch)."""
+    monkeypatch.setenv("MI_CKSUM_TX_BLOCKS", "1" if request.param == "blocks" else "0")
+    return request.param
 
 
 def dev(a):

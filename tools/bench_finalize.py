@@ -5,7 +5,7 @@ prepared handle, K back-to-back passes alternating over 2 streams, R rotating
 batches with >= 2 GiB read between two uses of one).  One JSON line per
 (config, op): GPU span per pass, algorithmic bytes = datagram bytes read + the
 op's bytes written (finalize: 4 B, verify: 5 B per datagram), fraction of the
-8 TB/s spec peak.  MI_CKSUM_TX_BLOCKS=0 selects the byte-store finalize (A/B).
+8 TB/s spec peak.  MI_CKSUM_TX_BLOCKS=1 selects the whole-block finalize stores (A/B).
 
     python tools/bench_finalize.py [--configs 1500,9000,pareto,64] [--steps 400]
 """
@@ -61,10 +61,11 @@ def main():
     ap.add_argument("--configs", default="1500,9000,pareto,64")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--ops", default="finalize,verify", help="order of the measured ops (A/A: verify,verify)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    blocks = os.environ.get("MI_CKSUM_TX_BLOCKS", "1") != "0"
+    blocks = os.environ.get("MI_CKSUM_TX_BLOCKS", "0") == "1"
     for cfg in a.configs.split(","):
         bs, n, lsum = make_batches(cfg, dev)
         outs = [dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
@@ -74,7 +75,7 @@ def main():
         # one handle at a time: two live handles' streams can share a hardware
         # queue (GPU_MAX_HW_QUEUES = 4) and serialise the 2-stream overlap
         for rnd in range(a.rounds):
-            for op in ("finalize", "verify"):
+            for op in a.ops.split(","):
                 rep = mi.VerifyRepeat(bs, outs if op == "verify" else None, nstreams=2, op=op)
                 rep.run(1000)
                 rep.run(a.steps, timed=True)

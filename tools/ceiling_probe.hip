@@ -40,6 +40,44 @@ __global__ __launch_bounds__(256) void rd_env(const uint8_t *p, uint32_t bytes, 
   if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads; practically never stores
 }
 
+// The same read plus in-place writes, to price TX finalize's stores alone:
+// WMODE 1: the lane holding chunk 0 of a slot stores 4 bytes into it (the
+// ip_sum / L4 sum patch of in_delayed_cksum + ip_sum); WMODE 2: the lanes
+// holding chunks 0..3 store them back whole (one full 64 B block per slot);
+// WMODE 3: 4 bytes per slot into a separate dense array (what verify writes).
+template <int U, int WMODE>
+__global__ __launch_bounds__(256) void rdw_env(uint8_t *p, uint32_t bytes, uint32_t nslots, uint32_t stride,
+                                              uint32_t env_off, uint32_t nch, uint32_t *side) {
+  auto r = __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
+  const uint32_t nthr = gridDim.x * 256u;
+  const uint32_t total = nslots * nch;
+  uint32_t acc = 0;  // every load is consumed (a load used only under a branch may be sunk into it)
+  for (uint32_t c = blockIdx.x * 256u + threadIdx.x; c < total; c += nthr * U) {
+    u32x4 v[U];
+    uint32_t slot[U], k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      slot[u] = cc / nch;
+      k[u] = cc - slot[u] * nch;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, cc < total ? slot[u] * stride + env_off + 16u * k[u] : 0xFFFFF000u,
+                                                   0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      if (cc >= total) continue;
+      const uint32_t a = slot[u] * stride + env_off + 16u * k[u];
+      const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+      acc += x;
+      if (WMODE == 1 && k[u] == 0) __builtin_amdgcn_raw_buffer_store_b32(x | 1u, r, a + 8u, 0, 0);
+      if (WMODE == 2 && k[u] < 4) __builtin_amdgcn_raw_buffer_store_b128(v[u], r, a, 0, 0);
+      if (WMODE == 3 && k[u] == 0) side[slot[u]] = x;
+    }
+  }
+  if (acc == 0x9E3779B9u) side[0] = acc;
+}
+
 template <int U>
 __global__ __launch_bounds__(256) void rd_flat(const uint8_t *p, uint32_t bytes, uint32_t *sink) {
   auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), 0, (int)bytes, 0x00020000);
@@ -66,8 +104,10 @@ extern "C" {
 // or a negative value on error.
 float ceil_run(void *const *bases, int nb, uint32_t bytes, uint32_t nslots, uint32_t stride, uint32_t env_off,
                uint32_t nch, int mode, int unroll, int grid, int steps, int nstreams) {
-  static uint32_t *sink = nullptr;
+  static uint32_t *sink = nullptr, *side = nullptr;
   if (!sink && hipMalloc(&sink, 256) != hipSuccess) return -1.f;
+  if (!side && hipMalloc(&side, 64u << 20) != hipSuccess) return -1.f;  // >= 4 B per slot of any batch
+  if (nslots > (16u << 20)) return -2.f;
   if (nstreams < 1 || nstreams > 8 || nb < 1) return -2.f;
   hipStream_t s[8];
   hipEvent_t e0, e1[8];
@@ -80,13 +120,19 @@ float ceil_run(void *const *bases, int nb, uint32_t bytes, uint32_t nslots, uint
   for (int q = 1; q < nstreams; ++q) hipStreamWaitEvent(s[q], e0, 0);
   const uint32_t flat = nslots * nch * 16u;
   for (int k = 0; k < steps; ++k) {
-    const uint8_t *p = (const uint8_t *)bases[k % nb];
+    uint8_t *p = (uint8_t *)bases[k % nb];
     hipStream_t st = s[k % nstreams];
 #define L(U)                                                                                         \
   if (mode == 0)                                                                                     \
-    hipLaunchKernelGGL((rd_env<U>), dim3(grid), dim3(256), 0, st, p, bytes, nslots, stride, env_off, nch, sink); \
+    hipLaunchKernelGGL((rd_env<U>), dim3(grid), dim3(256), 0, st, (const uint8_t *)p, bytes, nslots, stride, env_off, nch, sink); \
+  else if (mode == 1)                                                                                \
+    hipLaunchKernelGGL((rd_flat<U>), dim3(grid), dim3(256), 0, st, (const uint8_t *)p, flat, sink);                  \
+  else if (mode == 2)                                                                                \
+    hipLaunchKernelGGL((rdw_env<U, 1>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+  else if (mode == 3)                                                                                \
+    hipLaunchKernelGGL((rdw_env<U, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
   else                                                                                               \
-    hipLaunchKernelGGL((rd_flat<U>), dim3(grid), dim3(256), 0, st, p, flat, sink);
+    hipLaunchKernelGGL((rdw_env<U, 3>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side);
     if (unroll == 2) { L(2) } else if (unroll == 4) { L(4) } else if (unroll == 8) { L(8) } else { L(16) }
 #undef L
   }
