@@ -1660,8 +1660,12 @@ __device__ __forceinline__ u32x4 tx_build(const TxSegs &g, const TxCut &c, const
   return v;
 }
 
+// U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
+// prefetch costs ~10 and a few spill to scratch): profiles/tx_copy_r02.jsonl,
+// socket frames 59-64 us per launch against 64-66 without the prefetch and
+// 69 with it at 3 waves per SIMD.
 template <int G, int U>
-__global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
+__global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) {
   static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
   __shared__ uint32_t s_seg[kBlock / G][kTxSeg][2];
   Desc ds{}, dd{};
@@ -1673,9 +1677,51 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
   const int lane = threadIdx.x & (G - 1);
   const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
-  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < t.n; i += stride) {
-    const uint32_t len = t.pkt_len[i];
-    const uint32_t k0 = t.pkt_seg[i], k1 = t.pkt_seg[i + 1];
+  // Descriptor prefetch: a frame's descriptors are a chain of two dependent
+  // loads (pkt_seg -> seg_len / seg_off) ahead of its first data load, so the
+  // NEXT frame's chain is walked while this frame's data is in flight -- the
+  // first level at the top of the iteration, the second level right after this
+  // frame's first data pass is issued (its wait then covers only the older
+  // descriptor loads; vmcnt is in order).  Lane j holds segment k0 + j.
+  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  uint32_t len_c = 0, k0_c = 0, k1_c = 0;
+  int32_t sl_c = 0;
+  uint32_t so_c = 0;
+  if (i < t.n) {
+    len_c = t.pkt_len[i];
+    k0_c = t.pkt_seg[i];
+    k1_c = t.pkt_seg[i + 1];
+    if (k0_c + lane < k1_c) {
+      sl_c = t.seg_len[k0_c + lane];
+      so_c = (uint32_t)t.seg_off[k0_c + lane];
+    }
+  }
+  for (; i < t.n; i += stride) {
+    const uint32_t len = len_c;
+    const uint32_t k0 = k0_c, k1 = k1_c;
+    const int32_t sl0 = sl_c;
+    const uint32_t so0 = so_c;
+    const uint32_t in = i + stride;
+    uint32_t len_n = 0, k0_n = 0, k1_n = 0;
+    if (in < t.n) {
+      len_n = t.pkt_len[in];
+      k0_n = t.pkt_seg[in];
+      k1_n = t.pkt_seg[in + 1];
+    }
+    bool pre2 = false;
+    auto prefetch2 = [&]() {
+      if (pre2) return;
+      pre2 = true;
+      sl_c = 0;
+      so_c = 0;
+      if (in < t.n && k0_n + lane < k1_n) {
+        sl_c = t.seg_len[k0_n + lane];
+        so_c = (uint32_t)t.seg_off[k0_n + lane];
+      }
+      len_c = len_n;
+      k0_c = k0_n;
+      k1_c = k1_n;
+    };
     const uint32_t l3 = t.l3;
     const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
     const uint32_t h = D & 15u, c0 = D & ~15u;
@@ -1686,7 +1732,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
     uint32_t total = 0, ip_mlen = 0, m = 0;
     for (uint32_t w = k0; w < k1 && !st; w += G) {
       const uint32_t k = w + lane;
-      const uint32_t l = k < k1 ? (uint32_t)max(t.seg_len[k], 0) : 0u;
+      const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : t.seg_len[k], 0) : 0u;
       const uint32_t inc = group_scan<G>(l);
       const uint32_t a = total + inc - l, e = total + inc;
       const uint32_t nz = l ? 1u : 0u;
@@ -1694,7 +1740,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
       const uint32_t idx = m + zi - nz;
       if (nz && idx < (uint32_t)kTxSeg) {
         s_seg[grp][idx][0] = a;
-        s_seg[grp][idx][1] = (uint32_t)t.seg_off[k] - a;
+        s_seg[grp][idx][1] = (w == k0 ? so0 : (uint32_t)t.seg_off[k]) - a;
       }
       const bool isip = l && a <= l3 && l3 < e;
       ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
@@ -1704,6 +1750,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
     if (!st && total < len) st = MI_TX_SHORT;
     if (st) {
       if (lane == 0) t.status[i] = (uint8_t)st;
+      prefetch2();
       continue;
     }
     ip_mlen = group_lane<G>(ip_mlen, 0);
@@ -1771,6 +1818,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
           xa[u] = ld16(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
           xb[u] = ld16(rs, c.two && !c.slow ? c.A2 : kOOB);
         }
+        if (p == 0) prefetch2();
 #pragma unroll
         for (int u = 0; u < U; ++u)
           v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
@@ -1812,6 +1860,7 @@ __global__ __launch_bounds__(kBlock) void k_tx_copy(TxDesc t) {
       }
       __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
     }
+    prefetch2();
 #ifndef TX_NO_GENERIC
     if (!done) {
       // ---- generic path (long chains, an IP header split over mbufs, sum
