@@ -237,6 +237,17 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);
 int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_sum,
                          uint8_t *status, uint32_t *bad_count, void *stream);
 
+/*
+ * mi_cksum_ipv4_verify over nb <= 16 batches in ONE launch (same semantics per
+ * batch; ip / l4 / status: arrays of nb device pointers, any may be NULL;
+ * bad_count one device counter for all).  For a single RX queue with several
+ * bursts queued: the grid's ramp-up and drain are paid once, not per batch.
+ * Batches whose plan is not the lane-group kernel (packed, 64 B slots,
+ * length classes) are verified by one launch each, with the same results.
+ */
+int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4,
+                               uint8_t *const *status, uint32_t *bad_count, void *stream);
+
 /* Diagnostics: the verify kernel mi_cksum_ipv4_verify launches for this batch
  * ("k_ipv4_verify_packed<4>", "k_ipv4_verify<16,6>", ...).  Thread-local
  * string, valid until the next call.  Needs no GPU. */

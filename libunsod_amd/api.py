@@ -173,6 +173,19 @@ def ipv4_verify(b: PktBatch, *, ip: bool = True, l4: bool = True, status: bool =
     return res
 
 
+def ipv4_verify_multi(batches, outs, *, bad=None, stream=None) -> None:
+    """RX verify of several batches in one launch (mi_cksum_ipv4_verify_multi):
+    outs[k] = dict(ip, l4, status) device tensors for batches[k]; ``bad``: an
+    int32[1] device counter for all of them (or None)."""
+    nb = len(batches)
+    arr = (PktBatchC * nb)(*[b.c for b in batches])
+    VP = C.c_void_p * nb
+    ptrs = {k: VP(*[_ptr(o.get(k)) for o in outs]) for k in ("ip", "l4", "status")}
+    check("mi_cksum_ipv4_verify_multi",
+          load().mi_cksum_ipv4_verify_multi(arr, nb, ptrs["ip"], ptrs["l4"], ptrs["status"], _ptr(bad),
+                                            C.c_void_p(_stream(stream))))
+
+
 def verify_plan(b: PktBatch) -> str:
     """Name of the verify kernel ``ipv4_verify`` launches for ``b`` (diagnostics)."""
     return load().mi_cksum_verify_plan(C.byref(b.c)).decode()
@@ -492,6 +505,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
+    "ipv4_verify_host", "ipv4_verify_multi", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

@@ -643,6 +643,52 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
   if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
 
+// RX verify of SEVERAL batches in one launch (mi_cksum_ipv4_verify_multi): a
+// single RX queue with bursts queued submits them together, so the grid's
+// ramp-up and drain are paid once instead of per batch.  The work unit is one
+// wave's worth of datagrams (64 / G, one per lane group) of ONE batch, so the
+// batch -- and with it the buffer resource -- is uniform per wave (scalar
+// loads of the kernel-argument table, no waterfall).
+constexpr int kMaxMulti = 16;
+struct MultiEnt {
+  Desc d;
+  uint16_t *ip, *l4;
+  uint8_t *st;
+  uint32_t unit0;  // first unit of this batch
+  uint32_t pad;
+};
+struct MultiArgs {
+  uint32_t nb, units;
+  uint32_t *bad;
+  MultiEnt e[kMaxMulti];
+};
+
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_multi(MultiArgs a) {
+  constexpr uint32_t gpw = 64u / G;
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t gid = (threadIdx.x & 63u) / G;
+  const uint32_t nwaves = gridDim.x * (kBlock / 64);
+  for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
+    uint32_t j = 0;
+    for (uint32_t k = 1; k < a.nb; ++k) j = a.e[k].unit0 <= u ? k : j;
+    const Desc &d = a.e[j].d;
+    const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+    const uint32_t i = (u - a.e[j].unit0) * gpw + gid;
+    if (i >= d.n) continue;  // the batch's last unit: whole groups drop out
+    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    u32x4 v[U];
+    issue_first<G, U>(r, off, flen, lane, v);
+    IpHdr ih;
+    bool hdr_ok, l4_ok;
+    uint32_t sum_h, sum_l;
+    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    if (lane == 0)
+      verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
+                  a.e[j].ip, a.e[j].l4, a.e[j].st, a.bad, d);
+  }
+}
+
 // RX verify of a PACKED batch (MI_BATCH_PACKED: datagrams laid out close
 // together in ascending order -- the mixed-length Pareto layout).
 //
@@ -2513,6 +2559,60 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (!d.n) return 0;
   return launch_verify(d, batch_max_len(b), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
+}
+
+int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4,
+                               uint8_t *const *status, uint32_t *bad_count, void *stream) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b || !nb) return set_err(-EINVAL, "no batches");
+  if (nb > (uint32_t)kMaxMulti) return set_err(-EINVAL, "at most %d batches per launch", kMaxMulti);
+  hipStream_t s = (hipStream_t)stream;
+  MultiArgs a{};
+  a.bad = bad_count;
+  uint32_t ml = 0;
+  bool merge = true;
+  Desc d[kMaxMulti];
+  for (uint32_t k = 0; k < nb; ++k) {
+    if ((rc = make_desc(&b[k], &d[k]))) return rc;
+    const uint32_t m = batch_max_len(&b[k]);
+    ml = m > ml ? m : ml;
+    merge = merge && verify_plan(d[k], m).kind == kPlanShape;
+  }
+  if (!merge) {  // flat-run / slot / length-class plans: one launch per batch (same results)
+    for (uint32_t k = 0; k < nb; ++k)
+      if (d[k].n && (rc = launch_verify(d[k], batch_max_len(&b[k]), ip ? ip[k] : nullptr, l4 ? l4[k] : nullptr,
+                                         status ? status[k] : nullptr, bad_count, s)))
+        return rc;
+    return 0;
+  }
+  const Shape sh = pick_shape(ml);
+  const uint32_t gpw = 64u / (uint32_t)sh.g;
+  uint32_t units = 0;
+  for (uint32_t k = 0; k < nb; ++k) {
+    a.e[k].d = d[k];
+    a.e[k].ip = ip ? ip[k] : nullptr;
+    a.e[k].l4 = l4 ? l4[k] : nullptr;
+    a.e[k].st = status ? status[k] : nullptr;
+    a.e[k].unit0 = units;
+    const uint64_t u = ((uint64_t)d[k].n + gpw - 1) / gpw;
+    if (units + u > 0xffffffffull) return set_err(-E2BIG, "too many datagrams in one launch");
+    units += (uint32_t)u;
+  }
+  a.nb = nb;
+  a.units = units;
+  if (!units) return 0;
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 2048;
+  uint64_t blocks = ((uint64_t)units + (kBlock / 64) - 1) / (kBlock / 64);
+  if (blocks > (uint64_t)cap) blocks = cap;
+#define X(G_, U_)                                                                                 \
+  if (sh.g == G_ && sh.u == U_) {                                                                 \
+    VLAUNCH((k_ipv4_verify_multi<G_, U_>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);       \
+    return launched();                                                                            \
+  }
+  FOR_GU(X)
+#undef X
+  return set_err(-EINVAL, "no kernel for shape %dx%d", sh.g, sh.u);
 }
 
 const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {

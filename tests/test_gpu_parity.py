@@ -683,3 +683,54 @@ def test_offs32_same_results(golden, layout):
                      lens=dev_tensor(g["vb_flen"].astype(np.int32)), packed=True, offs32=True)
     mi.ipv4_finalize(gf)
     assert np.array_equal(cpu(gbuf), g["fin_out"])
+
+
+@pytest.mark.parametrize("shape", ["", "8x12"])
+def test_verify_multi_matches_single(shape):
+    """mi_cksum_ipv4_verify_multi == mi_cksum_ipv4_verify per batch: slot
+    batches of several lengths (merged into one launch), a packed batch (its
+    own launch), empty and one-packet batches, corrupted datagrams."""
+    if shape:
+        mi.set_shape(*[int(x) for x in shape.split("x")])
+    try:
+        rng = np.random.default_rng(404)
+        batches, outs, want = [], [], []
+        specs = [(3000, 1500, 2176, 142), (1, 1500, 2176, 142), (0, 1500, 2176, 142), (777, 9000, 9216, 142),
+                 (2500, 600, 640, 2), (4096, 1500, 2176, 143)]
+        for n, L, stride, first in specs:
+            b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=n + L, payload="pattern")
+            h = b0["buf"] if n else np.zeros(4096, np.uint8)
+            if n:
+                ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+                for i in rng.choice(n, max(1, n // 50), replace=False):
+                    h[first + int(i) * stride + int(rng.integers(0, L))] ^= 0x22
+            want.append(ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L) if n else None)
+            batches.append(mi.PktBatch(dev_tensor(h), n, stride=stride, first_off=first, fixed_len=L))
+            outs.append(dict(ip=torch.zeros(max(n, 1), dtype=torch.uint16, device="cuda"),
+                             l4=torch.zeros(max(n, 1), dtype=torch.uint16, device="cuda"),
+                             status=torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")))
+        lens = synth.pareto_lengths(3000, seed=5)
+        offs = synth.packed_offsets(lens, first_off=2)
+        bp = synth.build_ipv4_batch(3000, lens, offs=offs.astype(np.int64), seed=6)
+        hp = bp["buf"]
+        ORC.ipv4_finalize_batch(hp, 3000, offs=offs, flen=lens.astype(np.uint32))
+        hp[offs[::37].astype(np.int64) + 21] ^= 1
+        want.append(ORC.ipv4_verify_batch(hp, 3000, offs=offs, flen=lens.astype(np.uint32)))
+        batches.append(mi.PktBatch(dev_tensor(hp), 3000, offs=dev_tensor(offs.astype(np.int64)),
+                                   lens=dev_tensor(lens.astype(np.int32)), packed=True))
+        outs.append(dict(ip=torch.zeros(3000, dtype=torch.uint16, device="cuda"),
+                         l4=torch.zeros(3000, dtype=torch.uint16, device="cuda"),
+                         status=torch.zeros(3000, dtype=torch.uint8, device="cuda")))
+        bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+        mi.ipv4_verify_multi(batches, outs, bad=bad)
+        torch.cuda.synchronize()
+        nbad = 0
+        for w, o, b in zip(want, outs, batches):
+            if w is None:
+                continue
+            assert np.array_equal(cpu(o["ip"])[:b.n], w[0]) and np.array_equal(cpu(o["l4"])[:b.n], w[1])
+            assert np.array_equal(cpu(o["status"])[:b.n], w[2])
+            nbad += int((w[2] != 0).sum())
+        assert int(bad.item()) == nbad
+    finally:
+        mi.set_shape(0, 0, 0)
