@@ -405,7 +405,8 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
   if (i >= d.n) return;
   if constexpr (U > 4) {
     // wide shapes already keep U loads per lane in flight; double-buffering
-    // them would cost occupancy (8x12: 121 -> 172 VGPRs)
+    // them costs occupancy and measured slower (16x6: 91 -> 111 VGPRs, 2-stream
+    // 15.7 -> 16.5 us per 1500 B batch, profiles/db6_r02.jsonl; 8x12: 121 -> 172)
     for (; i < d.n; i += stride) {
       const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
       u32x4 v[U];
@@ -669,12 +670,28 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_multi(MultiArgs a) {
   const int lane = threadIdx.x & (G - 1);
   const uint32_t gid = (threadIdx.x & 63u) / G;
   const uint32_t nwaves = gridDim.x * (kBlock / 64);
+  // A wave's units only move forward, so its batch does too: the batch's
+  // descriptor is copied out of the argument table once per batch change, not
+  // re-read (a scalar-load round trip ahead of the data loads) per unit.
+  uint32_t j = 0, u0 = a.e[0].unit0;
+  uint32_t next = a.nb > 1 ? a.e[1].unit0 : 0xffffffffu;
+  Desc d = a.e[0].d;
+  uint16_t *ipo = a.e[0].ip, *l4o = a.e[0].l4;
+  uint8_t *sto = a.e[0].st;
   for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
-    uint32_t j = 0;
-    for (uint32_t k = 1; k < a.nb; ++k) j = a.e[k].unit0 <= u ? k : j;
-    const Desc &d = a.e[j].d;
+    if (u >= next) {
+      do {
+        ++j;
+      } while (j + 1 < a.nb && a.e[j + 1].unit0 <= u);
+      d = a.e[j].d;
+      u0 = a.e[j].unit0;
+      next = j + 1 < a.nb ? a.e[j + 1].unit0 : 0xffffffffu;
+      ipo = a.e[j].ip;
+      l4o = a.e[j].l4;
+      sto = a.e[j].st;
+    }
     const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
-    const uint32_t i = (u - a.e[j].unit0) * gpw + gid;
+    const uint32_t i = (u - u0) * gpw + gid;
     if (i >= d.n) continue;  // the batch's last unit: whole groups drop out
     const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
     u32x4 v[U];
@@ -685,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_multi(MultiArgs a) {
     ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0)
       verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
-                  a.e[j].ip, a.e[j].l4, a.e[j].st, a.bad, d);
+                  ipo, l4o, sto, a.bad, d);
   }
 }
 
