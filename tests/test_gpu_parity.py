@@ -734,3 +734,50 @@ def test_verify_multi_matches_single(shape):
         assert int(bad.item()) == nbad
     finally:
         mi.set_shape(0, 0, 0)
+
+
+def test_repeat_handle_outputs_and_rotation():
+    """mi_cksum_repeat_*: every pass writes exactly what mi_cksum_ipv4_verify
+    writes for its batch; runs continue the batch rotation; timed runs give a
+    positive span; the finalize op equals mi_cksum_ipv4_finalize; busy-wait
+    mode changes nothing but the wait."""
+    n, L, stride, first = 2048, 1500, 2176, 142
+    bs, outs, want = [], [], []
+    for r in range(3):
+        b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=90 + r)
+        h = b0["buf"]
+        ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+        h[first + (7 * r + 3) * stride + 200] ^= 0x80
+        want.append(ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L))
+        bs.append(mi.PktBatch(dev_tensor(h), n, stride=stride, first_off=first, fixed_len=L))
+        outs.append(dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                         l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                         status=torch.zeros(n, dtype=torch.uint8, device="cuda")))
+    mi.set_busy_wait(True)
+    try:
+        for ns in (1, 2, 3):
+            rep = mi.VerifyRepeat(bs, outs, nstreams=ns)
+            for o in outs:
+                for t in o.values():
+                    t.zero_()
+            torch.cuda.synchronize()
+            rep.run(2)  # batches 0, 1
+            assert not cpu(outs[2]["status"]).any() and not cpu(outs[2]["ip"]).any()
+            rep.run(1, timed=True)  # batch 2: the rotation continues
+            assert rep.span() > 0
+            rep.close()
+            for w, o in zip(want, outs):
+                assert np.array_equal(cpu(o["ip"]), w[0]) and np.array_equal(cpu(o["l4"]), w[1])
+                assert np.array_equal(cpu(o["status"]), w[2])
+    finally:
+        mi.set_busy_wait(False)
+    # finalize op: one pass per batch over fresh TX seeds == the oracle's finalize
+    b1 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=77)
+    ref = b1["buf"].copy()
+    ORC.ipv4_finalize_batch(ref, n, stride=stride, first_off=first, fixed_flen=L)
+    buf = dev_tensor(b1["buf"])
+    fb = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
+    rep = mi.VerifyRepeat([fb], None, nstreams=2, op="finalize")
+    rep.run(1)
+    rep.close()
+    assert np.array_equal(cpu(buf), ref)
