@@ -1527,10 +1527,18 @@ __device__ __forceinline__ void put_byte(u32x4 &v, int b, uint32_t x) {
   v.w = j == 3 ? (v.w & m) | y : v.w;
 }
 // Store bytes [lo, hi) of chunk v at destination address a (16-aligned).
+// Copied frames are written once and not read back by this kernel:
+// nontemporal stores (aux = 2, `nt`) lift a plain slot copy of the TX
+// geometry from 0.51 to 0.62 of HBM (tools/ceiling_copy.py,
+// profiles/ceiling_copy_r02.jsonl).
+#ifndef MI_TX_STORE_AUX
+#define MI_TX_STORE_AUX 2
+#endif
 __device__ __forceinline__ void store_chunk(__amdgpu_buffer_rsrc_t r, uint32_t a, const u32x4 &v, int lo,
                                             int hi) {
+  constexpr int kAux = MI_TX_STORE_AUX;
   if (lo <= 0 && hi >= 16) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, a, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, a, 0, kAux);
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -1538,10 +1546,10 @@ __device__ __forceinline__ void store_chunk(__amdgpu_buffer_rsrc_t r, uint32_t a
   for (int j = 0; j < 4; ++j) {
     const int b0 = min(max(lo - 4 * j, 0), 4), b1 = min(max(hi - 4 * j, 0), 4);
     if (b0 == 0 && b1 == 4) {
-      __builtin_amdgcn_raw_buffer_store_b32(w[j], r, a + 4u * j, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(w[j], r, a + 4u * j, 0, kAux);
     } else {
       for (int m = b0; m < b1; ++m)
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j] >> (8 * m)), r, a + 4u * j + m, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j] >> (8 * m)), r, a + 4u * j + m, 0, kAux);
     }
   }
 }
@@ -1680,19 +1688,21 @@ struct TxCut {
   bool two, clip, slow;
 };
 __device__ __forceinline__ TxCut tx_cut(const TxSegs &g, uint32_t ci, uint32_t h) {
+  const int S1 = g.S1, S2 = g.S2, S3 = g.S3, L = g.L;
+  const uint32_t D0 = g.D0, D1 = g.D1, D2 = g.D2, D3 = g.D3;
   TxCut c;
   c.q0 = (int)(16u * ci) - (int)h;
-  const int q = max(c.q0, 0), hi = min(c.q0 + 16, g.L);
-  const bool j1 = q >= g.S1, j2 = q >= g.S2, j3 = q >= g.S3;
-  const uint32_t d0 = j3 ? g.D3 : j2 ? g.D2 : j1 ? g.D1 : g.D0;
-  const uint32_t d1 = j2 ? g.D3 : j1 ? g.D2 : g.D1;
-  const int s1 = j3 ? g.L : j2 ? g.S3 : j1 ? g.S2 : g.S1;
-  const int s2 = j2 ? g.L : j1 ? g.S3 : g.S2;
+  const int q = max(c.q0, 0), hi = min(c.q0 + 16, L);
+  const bool j1 = q >= S1, j2 = q >= S2, j3 = q >= S3;
+  const uint32_t d0 = j3 ? D3 : j2 ? D2 : j1 ? D1 : D0;
+  const uint32_t d1 = j2 ? D3 : j1 ? D2 : D1;
+  const int s1 = j3 ? L : j2 ? S3 : j1 ? S2 : S1;
+  const int s2 = j2 ? L : j1 ? S3 : S2;
   c.A1 = (uint32_t)c.q0 + d0;
   c.A2 = (uint32_t)c.q0 + d1;
   c.B = s1 - c.q0;
   c.two = s1 < hi;
-  c.clip = c.q0 < 0 || c.q0 + 16 > g.L;
+  c.clip = c.q0 < 0 || c.q0 + 16 > L;
   c.slow = q < hi && (c.A1 > g.lim || (c.two && (s2 < hi || c.A2 > g.lim)));
   return c;
 }
@@ -1721,6 +1731,101 @@ __device__ __forceinline__ u32x4 tx_build(const TxSegs &g, const TxCut &c, const
     }
   }
   return v;
+}
+
+// What ip_output decides for a frame from its IP header and m_pkthdr
+// (ip_output.c:649-672 with in_delayed_cksum, ip_output.c:958-983): which sums
+// to do, where the L4 one goes (at = hl + csum_data), and whether the datagram
+// is well-formed enough to be summed at all.
+struct TxPlan {
+  bool ok, do_ip, do_l4, udp;
+  uint32_t at;
+  int hend, lend;  // header / datagram length when ok, else 0
+};
+__device__ __forceinline__ TxPlan tx_plan(const TxDesc &t, uint32_t i, uint32_t len, const IpHdr &ih) {
+  TxPlan pl;
+  const uint32_t flen = len >= t.l3 ? len - t.l3 : 0u;
+  pl.ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl && ih.iplen <= flen;
+  const uint32_t fl =
+      t.cflags ? t.cflags[i] : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
+  pl.do_ip = pl.ok && (fl & MI_CSUM_IP);
+  pl.do_l4 = pl.ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
+  pl.udp = fl & MI_CSUM_UDP;
+  pl.at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? 16u : 6u);
+  pl.hend = pl.ok ? (int)ih.hl : 0;
+  pl.lend = pl.ok ? (int)ih.iplen : 0;
+  return pl;
+}
+__device__ __forceinline__ uint8_t tx_status(const TxPlan &pl, bool l4_store) {
+  return (uint8_t)((pl.ok ? 0u : MI_TX_NOSUM) | (pl.do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+}
+
+// Generic gather of frame i by a G-lane group (long chains, an IP header split
+// over mbufs, sum fields far from the header): chunk-major over the whole
+// frame, every piece of every chunk gathered by walking the chain; chunks
+// stored as they are built, the sum fields patched once they have landed.
+// len, the chain [k0, k1) and ip_mlen come from the caller's chain walk.
+template <int G, int U>
+__device__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, uint32_t i,
+                                 int lane, uint32_t len, uint32_t k0, uint32_t k1, uint32_t ip_mlen) {
+  const uint32_t l3 = t.l3;
+  const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
+  const uint32_t h = D & 15u, c0 = D & ~15u;
+  const bool odd = (h + l3) & 1u;
+  IpHdr ih{};
+  TxPlan pl{};
+  uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
+  const uint32_t nch = (h + len + 15u) >> 4;
+  const uint32_t npass = (nch + G * U - 1) / (G * U);
+  for (uint32_t p = 0; p < npass; ++p) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cs = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
+      v[u] = u32x4{0, 0, 0, 0};
+      int pos = 0;
+      for (uint32_t k = k0; k < k1; ++k) {
+        const int l = max(t.seg_len[k], 0);
+        const int lo = max(pos - cs, 0), hi = min(min(pos + l, (int)len) - cs, 16);
+        if (hi > lo) {
+          const uint32_t a = (uint32_t)cs + ((uint32_t)t.seg_off[k] - (uint32_t)pos);
+          merge_bytes(v[u], shift_pair(ld_pair(rs, a), a), lo, hi);
+        }
+        pos += l;
+      }
+    }
+    if (p == 0) {
+      const u32x4 hv[1] = {v[0]};
+      ih = parse_ipv4<G, 1>(hv, h + l3);
+      pl = tx_plan(t, i, len, ih);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t ci = p * (G * U) + u * G + lane;
+      const int cs = (int)(16u * ci) - (int)h;
+      fold_chunk(v[u], cs - (int)l3, pl.lend, pl.hend, pl.hend > 20, acc_t, acc_h, acc_f);
+      if (ci < nch) store_chunk(rd, c0 + 16u * ci, v[u], -cs, (int)len - cs);
+    }
+  }
+  if (npass == 0) pl = TxPlan{};
+  const bool l4_store = pl.do_l4 && (uint64_t)pl.at + 2u <= ip_mlen;
+  uint32_t c_ip, c_l4;
+  tx_sums<G>(acc_t, acc_h, acc_f, pl.hend, ih, odd, pl.udp, c_ip, c_l4);
+  if (pl.do_ip || l4_store) {
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's chunk stores have landed
+    if (lane == 0) {
+      const uint32_t pip = l3 + 10u, pl4 = l3 + pl.at;
+      if (pl.do_ip) {
+        if (pip < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_ip, rd, D + pip, 0, 0);
+        if (pip + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_ip >> 8), rd, D + pip + 1u, 0, 0);
+      }
+      if (l4_store) {
+        if (pl4 < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_l4, rd, D + pl4, 0, 0);
+        if (pl4 + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_l4 >> 8), rd, D + pl4 + 1u, 0, 0);
+      }
+    }
+  }
+  if (lane == 0) t.status[i] = tx_status(pl, l4_store);
 }
 
 // U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
@@ -1826,16 +1931,14 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
     auto decide1 = [&](const u32x4 &h0, uint32_t hoff) {
       const u32x4 hv[1] = {h0};
       ih = parse_ipv4<G, 1>(hv, hoff);
-      const uint32_t flen = len >= l3 ? len - l3 : 0u;
-      ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl && ih.iplen <= flen;
-      const uint32_t fl = t.cflags ? t.cflags[i]
-                                   : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
-      do_ip = ok && (fl & MI_CSUM_IP);
-      do_l4 = ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
-      udp = fl & MI_CSUM_UDP;
-      at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? 16u : 6u);
-      hend = ok ? (int)ih.hl : 0;
-      lend = ok ? (int)ih.iplen : 0;
+      const TxPlan pl = tx_plan(t, i, len, ih);
+      ok = pl.ok;
+      do_ip = pl.do_ip;
+      do_l4 = pl.do_l4;
+      udp = pl.udp;
+      at = pl.at;
+      hend = pl.hend;
+      lend = pl.lend;
     };
     auto fold_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t p) {
 #pragma unroll
@@ -1875,16 +1978,17 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       for (uint32_t p = 0; p < npass; ++p) {
         u32x4 v[U];
         u32x4 xa[U], xb[U];
+        TxCut cut[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
           xa[u] = ld16(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
           xb[u] = ld16(rs, c.two && !c.slow ? c.A2 : kOOB);
+          cut[u] = c;
         }
         if (p == 0) prefetch2();
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
+        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
@@ -1925,56 +2029,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
     }
     prefetch2();
 #ifndef TX_NO_GENERIC
-    if (!done) {
-      // ---- generic path (long chains, an IP header split over mbufs, sum
-      // fields far from the header): chunk-major over the whole frame, every
-      // piece of every chunk gathered by walking the chain; chunks stored as
-      // they are built, the sum fields patched once they have landed.
-      acc_t = acc_h = acc_f = 0;
-      const uint32_t nch = (h + len + 15u) >> 4;
-      const uint32_t npass = (nch + G * U - 1) / (G * U);
-      for (uint32_t p = 0; p < npass; ++p) {
-        u32x4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int cs = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
-          v[u] = u32x4{0, 0, 0, 0};
-          int pos = 0;
-          for (uint32_t k = k0; k < k1; ++k) {
-            const int l = max(t.seg_len[k], 0);
-            const int lo = max(pos - cs, 0), hi = min(min(pos + l, (int)len) - cs, 16);
-            if (hi > lo) {
-              const uint32_t a = (uint32_t)cs + ((uint32_t)t.seg_off[k] - (uint32_t)pos);
-              merge_bytes(v[u], shift_pair(ld_pair(rs, a), a), lo, hi);
-            }
-            pos += l;
-          }
-        }
-        if (p == 0) decide1(v[0], h + l3);
-        fold_all(v, 0, p);
-        store_all(v, 0, nch, p, 0, (int)len);
-      }
-      if (npass == 0) ok = do_ip = do_l4 = false;
-      const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-      uint32_t c_ip, c_l4;
-      tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
-      if (do_ip || l4_store) {
-        __builtin_amdgcn_s_waitcnt(0);  // this wave's chunk stores have landed
-        if (lane == 0) {
-          const uint32_t pip = l3 + 10u, pl4 = l3 + at;
-          if (do_ip) {
-            if (pip < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_ip, rd, D + pip, 0, 0);
-            if (pip + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_ip >> 8), rd, D + pip + 1u, 0, 0);
-          }
-          if (l4_store) {
-            if (pl4 < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_l4, rd, D + pl4, 0, 0);
-            if (pl4 + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_l4 >> 8), rd, D + pl4 + 1u, 0, 0);
-          }
-        }
-      }
-      if (lane == 0)
-        t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
-    }
+    if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
 #endif
   }
 }
@@ -2449,21 +2504,18 @@ int launch_finalize(const Desc &d, Shape sh, hipStream_t s, uint32_t max_len) {
 #define FOR_TX_GU(X) X(8, 2) X(8, 4) X(8, 8) X(16, 2) X(16, 4) X(16, 6) X(16, 8) X(32, 2) X(32, 4) X(64, 2) X(64, 4)
 
 Shape pick_tx_shape(uint32_t max_len) {
-  static const Shape forced = [] {
-    Shape f{0, 0};
-    if (const char *e = getenv("MI_CKSUM_TX_SHAPE")) {
-      int g = 0, u = 0;
-      if (sscanf(e, "%dx%d", &g, &u) == 2) f = {g, u};
-    }
-    return f;
-  }();
-  if (forced.g) return forced;
+  // MI_CKSUM_TX_SHAPE "GxU": read per call so a test can switch shapes
+  if (const char *e = getenv("MI_CKSUM_TX_SHAPE")) {
+    int g = 0, u = 0;
+    if (sscanf(e, "%dx%d", &g, &u) == 2) return {g, u};
+  }
   // mi_cksum_set_shape applies when it names a TX shape
 #define X(G_, U_) if (g_tune.g == G_ && g_tune.u == U_) return {G_, U_};
   FOR_TX_GU(X)
 #undef X
   // the gather is latency-bound per frame: narrow groups (more frames in
-  // flight per wave) and short passes (occupancy) win -- profiles/tx_sweep_r01.jsonl
+  // flight per wave) and short passes (occupancy) win -- profiles/tx_sweep_r01.jsonl,
+  // profiles/tx_flat_r02.jsonl (a wave-flat layout over 4-32 frames lost to it)
   (void)max_len;
   return {8, 2};
 }

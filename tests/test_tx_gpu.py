@@ -52,6 +52,19 @@ def test_tx_every_shape(shape):
         mi.set_shape(0, 0, 0)
 
 
+@pytest.mark.parametrize("shape", ["8x2", "16x4", "64x2"])
+def test_tx_every_case_per_shape(shape, monkeypatch):
+    """Every edge case (padding, far headers, ragged counts included) through
+    a narrow, a middle and a whole-wave group shape (MI_CKSUM_TX_SHAPE)."""
+    monkeypatch.setenv("MI_CKSUM_TX_SHAPE", shape)
+    for name, c in CASES:
+        want_dst, want_st = run_oracle(ORC, c)
+        got_dst, got_st = run_gpu(c)
+        assert np.array_equal(got_st, want_st), (shape, name, np.nonzero(got_st != want_st)[0][:8])
+        bad = np.nonzero(got_dst != want_dst)[0]
+        assert bad.size == 0, (shape, name, bad.size, bad[:8])
+
+
 def test_tx_full_size_then_rx_verify():
     """65536 x 1514 B frames in socket-buffer chains -> rte_mbuf slots; the
     slots then verify to 0/0 on the GPU RX path."""

@@ -43,6 +43,23 @@ def test_tx_status_rules():
     assert np.array_equal(st == 8, big)  # the sum field beyond the IP mbuf: "delayed m_pullup"
 
 
+@pytest.mark.parametrize("name", ["eth-padding", "eth-padding-socket", "l3-64-hl-60", "ragged-count-mixed"])
+def test_tx_new_cases_verify(name):
+    """The padded / far-header / ragged cases are summed (status 0 where the
+    IP mbuf holds the L4 field) and their frames verify to 0/0."""
+    c = dict(edge_cases(PORT))[name]
+    dst, st = run_oracle(PORT, c)
+    n = len(c["pkt_len"])
+    assert set(np.unique(st)) <= {0, 8} and (st == 0).sum() >= n // 2
+    flen = c["pkt_len"].astype(np.int64) - c["l3"]
+    ip, l4, vs = PORT.ipv4_verify_batch(dst, n, stride=c["stride"], first_off=c["dst_first"] + c["l3"], flen=flen)
+    assert not ip.any()
+    assert np.array_equal(vs != 0, st == 8)
+    if name.startswith("eth-padding"):
+        ip_len = np.array([int(f[c["l3"] + 2]) << 8 | int(f[c["l3"] + 3]) for f in c["frames"]])
+        assert (ip_len < flen).sum() >= n // 2  # padding really follows most datagrams
+
+
 def test_tx_zero_udp_sum_stored_as_ffff():
     c = dict(edge_cases(PORT))["zero-udp-sum"]
     dst, st = run_oracle(PORT, c)

@@ -85,7 +85,31 @@ def edge_cases(orc) -> list[tuple[str, dict]]:
     d = make_case(8, 1500, layout="socket", seed=22)
     out.append(("many-segments", _resegment(d, 40)))
     out.append(("zero-udp-sum", zero_udp_sum_case(orc)))
+    # Ethernet padding after the datagram (short frames padded to 60 B, and
+    # a few full-size ones): the L4 sum must stop at ip_len
+    out.append(("eth-padding", _pad_frames(make_case(40, rng.integers(28, 47, 40), layout="single", proto=17,
+                                                     seed=23), rng.integers(0, 20, 40))))
+    out.append(("eth-padding-socket", _pad_frames(make_case(24, 1400, layout="socket", seed=24),
+                                                  rng.integers(1, 40, 24))))
+    # IP header and TCP sum far into the slot: l3 = 64, 60-byte IP header,
+    # 15 bytes into the first 16-byte chunk
+    out.append(("l3-64-hl-60", make_case(24, 900, layout="socket", seed=25, l3=64, hl=60, dst_first=15)))
+    # more frames than one wave's group, ragged count, mixed layouts' lengths
+    out.append(("ragged-count-mixed", make_case(203, rng.integers(20, 1500, 203), layout="socket", seed=26,
+                                                dst_first=7)))
     return out
+
+
+def _pad_frames(c: dict, pad) -> dict:
+    """Extend every frame's last mbuf by pad[i] bytes (whatever follows it in
+    the blob): pkt_len grows, the IP datagram does not."""
+    c = dict(c)
+    sl, pl = c["seg_len"].copy(), c["pkt_len"].copy()
+    for i in range(len(pl)):
+        sl[int(c["pkt_seg"][i + 1]) - 1] += int(pad[i])
+        pl[i] += int(pad[i])
+    c.update(seg_len=sl, pkt_len=pl)
+    return c
 
 
 def _resegment(c: dict, nseg: int) -> dict:

@@ -112,7 +112,7 @@ def main():
         b.record()
         torch.cuda.synchronize()
         iso.append(a.elapsed_time(b) * 1e3)
-    res.update(shape=args.shape or "auto", op="tx_copy (fused m_copydata + in_delayed_cksum + ip_sum)", layout=args.layout, frames=n,
+    res.update(shape=args.shape or os.environ.get("MI_CKSUM_TX_SHAPE", "auto"), op="tx_copy (fused m_copydata + in_delayed_cksum + ip_sum)", layout=args.layout, frames=n,
                frame_len=frame, segments_per_frame=round((len(c["seg_len"])) / n, 2), rotating=R,
                us_per_launch=round(us, 2), isolated_us=round(float(np.median(iso)), 2),
                frames_GiBps=round(n * frame / (us / 1e6) / 2**30, 1),

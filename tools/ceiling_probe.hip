@@ -12,6 +12,12 @@
 //           kernel's bytes without its arithmetic;
 //   mode 1  one contiguous run of the same byte count per batch (no slot
 //           gaps): the best case for the same traffic.
+//
+// ceil_copy (the TX copy's ceiling): chunk c of the flat
+// slot space is read at src slot * sstride + soff + 16 k (soff may be
+// misaligned: one unaligned 16-byte load, as k_tx_flat issues) and written at
+// dst slot * dstride + doff + 16 k -- the same bytes as the fused TX copy
+// without its gather arithmetic.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -97,7 +103,77 @@ __global__ __launch_bounds__(256) void rd_flat(const uint8_t *p, uint32_t bytes,
   if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+template <int U, int SAUX>
+__global__ __launch_bounds__(256) void cp_env(const uint8_t *src, uint32_t sbytes, uint8_t *dst, uint32_t dbytes,
+                                             uint32_t nslots, uint32_t sstride, uint32_t soff, uint32_t dstride,
+                                             uint32_t doff, uint32_t nch) {
+  auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src), 0, (int)sbytes, 0x00020000);
+  auto rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, (int)dbytes, 0x00020000);
+  const uint32_t nthr = gridDim.x * 256u;
+  const uint32_t total = nslots * nch;
+  for (uint32_t c = blockIdx.x * 256u + threadIdx.x; c < total; c += nthr * U) {
+    u32x4 v[U];
+    uint32_t slot[U], k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      slot[u] = cc / nch;
+      k[u] = cc - slot[u] * nch;
+      v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, cc < total ? slot[u] * sstride + soff + 16u * k[u] : 0xFFFFF000u,
+                                                   0, 2);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t cc = c + (uint32_t)u * nthr;
+      __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, cc < total ? slot[u] * dstride + doff + 16u * k[u] : 0xFFFFF000u,
+                                             0, SAUX);
+    }
+  }
+}
+
 extern "C" {
+
+// steps copy launches over (srcs[k % nb], dsts[k % nb]) alternating over
+// nstreams streams; returns the GPU span in us.
+float ceil_copy(void *const *srcs, void *const *dsts, int nb, uint32_t sbytes, uint32_t dbytes, uint32_t nslots,
+                uint32_t sstride, uint32_t soff, uint32_t dstride, uint32_t doff, uint32_t nch, int unroll, int grid,
+                int steps, int nstreams, int saux) {
+  if (nstreams < 1 || nstreams > 8 || nb < 1) return -2.f;
+  hipStream_t s[8];
+  hipEvent_t e0, e1[8];
+  for (int q = 0; q < nstreams; ++q) {
+    if (hipStreamCreateWithFlags(&s[q], hipStreamNonBlocking) != hipSuccess) return -3.f;
+    if (hipEventCreate(&e1[q]) != hipSuccess) return -3.f;
+  }
+  if (hipEventCreate(&e0) != hipSuccess) return -3.f;
+  hipEventRecord(e0, s[0]);
+  for (int q = 1; q < nstreams; ++q) hipStreamWaitEvent(s[q], e0, 0);
+  for (int k = 0; k < steps; ++k) {
+    const uint8_t *a = (const uint8_t *)srcs[k % nb];
+    uint8_t *b = (uint8_t *)dsts[k % nb];
+    hipStream_t st = s[k % nstreams];
+#define L(U, A) hipLaunchKernelGGL((cp_env<U, A>), dim3(grid), dim3(256), 0, st, a, sbytes, b, dbytes, nslots, sstride, soff, dstride, doff, nch);
+#define LA(U) if (saux == 0) { L(U, 0) } else if (saux == 1) { L(U, 1) } else if (saux == 2) { L(U, 2) } else { L(U, 3) }
+    if (unroll == 2) { LA(2) } else if (unroll == 4) { LA(4) } else { LA(8) }
+#undef LA
+#undef L
+  }
+  for (int q = 0; q < nstreams; ++q) hipEventRecord(e1[q], s[q]);
+  float span = 0.f;
+  for (int q = 0; q < nstreams; ++q) {
+    hipEventSynchronize(e1[q]);
+    float t = 0.f;
+    hipEventElapsedTime(&t, e0, e1[q]);
+    if (t > span) span = t;
+  }
+  if (hipGetLastError() != hipSuccess) span = -4.f / 1000.f;
+  for (int q = 0; q < nstreams; ++q) {
+    hipEventDestroy(e1[q]);
+    hipStreamDestroy(s[q]);
+  }
+  hipEventDestroy(e0);
+  return span * 1000.f;
+}
 
 // steps launches, launch k over bases[k % nb] on stream k % nstreams (created
 // here, non-blocking); returns the GPU span of all launches in us (events),
