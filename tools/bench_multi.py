@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="1500")
     ap.add_argument("--ms", default="1,2,4,8,16")
     ap.add_argument("--batches", type=int, default=320, help="batches verified per measurement")
+    ap.add_argument("--caps", default="0", help="workgroup caps to sweep (0: the library default, 2048)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L, stride, first = CFG[a.config]
@@ -46,7 +47,8 @@ def main():
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
     alg = n * L + 5 * n
-    for m in [int(x) for x in a.ms.split(",")]:
+    for cap, m in [(c, m) for c in [int(x) for x in a.caps.split(",")] for m in [int(x) for x in a.ms.split(",")]]:
+        mi.set_shape(0, 0, cap)
         launches = a.batches // m
 
         def go(k):
@@ -68,9 +70,12 @@ def main():
             e1.record(s)
         s.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / (launches * m)
-        print(json.dumps(dict(config=a.config, batches_per_launch=m, launches=launches, streams=1,
+        print(json.dumps(dict(config=a.config, batches_per_launch=m, launches=launches, streams=1, cap=cap or 2048,
                               us_per_batch=round(us, 3), frac=round(alg / us / 8e6, 4),
                               GiBps=round(n * L / (us * 1e-6) / 2**30, 1))), flush=True)
+
+
+    mi.set_shape(0, 0, 0)
 
 
 if __name__ == "__main__":

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void rd_env(const uint8_t *p, uint32_t bytes, 
 // ip_sum / L4 sum patch of in_delayed_cksum + ip_sum); WMODE 2: the lanes
 // holding chunks 0..3 store them back whole (one full 64 B block per slot);
 // WMODE 3: 4 bytes per slot into a separate dense array (what verify writes).
-template <int U, int WMODE>
+// SAUX: the stores' cache policy (2 = nontemporal).
+template <int U, int WMODE, int SAUX = 0>
 __global__ __launch_bounds__(256) void rdw_env(uint8_t *p, uint32_t bytes, uint32_t nslots, uint32_t stride,
                                               uint32_t env_off, uint32_t nch, uint32_t *side) {
   auto r = __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
@@ -76,12 +77,22 @@ __global__ __launch_bounds__(256) void rdw_env(uint8_t *p, uint32_t bytes, uint3
       const uint32_t a = slot[u] * stride + env_off + 16u * k[u];
       const uint32_t x = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
       acc += x;
-      if (WMODE == 1 && k[u] == 0) __builtin_amdgcn_raw_buffer_store_b32(x | 1u, r, a + 8u, 0, 0);
-      if (WMODE == 2 && k[u] < 4) __builtin_amdgcn_raw_buffer_store_b128(v[u], r, a, 0, 0);
+      if (WMODE == 1 && k[u] == 0) __builtin_amdgcn_raw_buffer_store_b32(x | 1u, r, a + 8u, 0, SAUX);
+      if (WMODE == 2 && k[u] < 4) __builtin_amdgcn_raw_buffer_store_b128(v[u], r, a, 0, SAUX);
       if (WMODE == 3 && k[u] == 0) side[slot[u]] = x;
     }
   }
   if (acc == 0x9E3779B9u) side[0] = acc;
+}
+
+// A write-only pass of the same in-place patches (no reads): 4 bytes at
+// slot * stride + env_off + 8 per slot -- the second half of a finalize split
+// into a read-only sum pass (sums to a side array) and a patch pass.
+__global__ __launch_bounds__(256) void wr_patch(uint8_t *p, uint32_t bytes, uint32_t nslots, uint32_t stride,
+                                               uint32_t env_off) {
+  auto r = __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)bytes, 0x00020000);
+  for (uint32_t s = blockIdx.x * 256u + threadIdx.x; s < nslots; s += gridDim.x * 256u)
+    __builtin_amdgcn_raw_buffer_store_b32(s | 1u, r, s * stride + env_off + 8u, 0, 0);
 }
 
 template <int U>
@@ -207,8 +218,14 @@ float ceil_run(void *const *bases, int nb, uint32_t bytes, uint32_t nslots, uint
     hipLaunchKernelGGL((rdw_env<U, 1>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
   else if (mode == 3)                                                                                \
     hipLaunchKernelGGL((rdw_env<U, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+  else if (mode == 4)                                                                                \
+    hipLaunchKernelGGL((rdw_env<U, 3>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+  else if (mode == 5)                                                                                \
+    hipLaunchKernelGGL((rdw_env<U, 1, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+  else if (mode == 6)                                                                                \
+    hipLaunchKernelGGL((rdw_env<U, 2, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
   else                                                                                               \
-    hipLaunchKernelGGL((rdw_env<U, 3>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side);
+    hipLaunchKernelGGL(wr_patch, dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off);
     if (unroll == 2) { L(2) } else if (unroll == 4) { L(4) } else if (unroll == 8) { L(8) } else { L(16) }
 #undef L
   }

@@ -9,6 +9,7 @@ R rotating batches (>= 2 GiB read between reuses).
 """
 from __future__ import annotations
 
+import argparse
 import ctypes as C
 import json
 import os
@@ -19,19 +20,27 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-CFG = {"1500": (65536, 1500, 2176, 142), "9000": (65536, 9000, 9216, 142)}
+# "packed288": a packed stand-in for the Pareto batch (4 Mi datagrams, ~288 B apart)
+CFG = {"1500": (65536, 1500, 2176, 142), "9000": (65536, 9000, 9216, 142), "packed288": (1 << 22, 284, 288, 2)}
 MODES = {0: "read only", 2: "read + 4 B in place per slot", 3: "read + 64 B block in place per slot",
-         4: "read + 4 B per slot to a side array"}
+         4: "read + 4 B per slot to a side array", 5: "read + 4 B in place per slot, nt store",
+         6: "read + 64 B block in place per slot, nt store", 7: "4 B in place per slot, write only"}
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1500,9000")
+    ap.add_argument("--modes", default=",".join(str(m) for m in MODES))
+    ap.add_argument("--streams", default="2,1")
+    a = ap.parse_args()
     lib = C.CDLL(os.path.join(ROOT, "tools", "libceiling.so"))
     lib.ceil_run.restype = C.c_float
     lib.ceil_run.argtypes = [C.POINTER(C.c_void_p), C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                              C.c_uint32, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     dev = torch.device("cuda", 0)
     K = 400
-    for cfg, (n, L, stride, first) in CFG.items():
+    for cfg in a.configs.split(","):
+        n, L, stride, first = CFG[cfg]
         size = (first + (n - 1) * stride + L + 64 + 255) & ~255
         env_off = first & ~15
         nch = (first + L + 15) // 16 - env_off // 16
@@ -39,8 +48,8 @@ def main():
         bufs = [torch.randint(0, 255, (size,), dtype=torch.uint8, device=dev) for _ in range(R)]
         bases = (C.c_void_p * R)(*[b.data_ptr() for b in bufs])
         torch.cuda.synchronize()
-        for ns in (2, 1):
-            for mode in MODES:
+        for ns in [int(x) for x in a.streams.split(",")]:
+            for mode in [int(x) for x in a.modes.split(",")]:
                 lib.ceil_run(bases, R, size, n, stride, env_off, nch, mode, 4, 8192, 200, ns)  # warm
                 sp = lib.ceil_run(bases, R, size, n, stride, env_off, nch, mode, 4, 8192, K, ns)
                 if sp <= 0:
