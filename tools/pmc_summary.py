@@ -3,6 +3,7 @@
 (rocpd SQLite, the `counters_collection` view), one JSON line per kernel.
 
     python tools/pmc_summary.py gpurun_out/pmc_tx_*/pmc_results.db [--match tx_]
+    python tools/pmc_summary.py --trace gpurun_out/txprof/trace/tx_results.db --match k_tx_copy
 """
 from __future__ import annotations
 
@@ -33,10 +34,37 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dbs", nargs="+")
     ap.add_argument("--match", default="")
+    ap.add_argument("--trace", action="store_true", help="the dbs are --kernel-trace databases: dispatch stats")
     a = ap.parse_args()
     for db in a.dbs:
+        if a.trace:
+            print(json.dumps(trace_union(db, a.match)))
+            continue
         for row in summarize(db, a.match):
             print(json.dumps(row))
+
+
+
+def trace_union(db: str, match: str):
+    """Per-kernel dispatch statistics from a rocprofv3 --kernel-trace database:
+    count, mean / min / max duration, and the union of the dispatch intervals
+    per dispatch (the GPU time per launch when launches overlap on 2 streams)."""
+    c = sqlite3.connect(db)
+    iv = sorted((s, e) for n, s, e in c.execute("select name, start, end from kernels") if match in n)
+    if not iv:
+        return None
+    union, cs, ce = 0, iv[0][0], iv[0][1]
+    for s, e in iv[1:]:
+        if s > ce:
+            union += ce - cs
+            cs, ce = s, e
+        else:
+            ce = max(ce, e)
+    union += ce - cs
+    d = [e - s for s, e in iv]
+    return dict(db=db, kernel=match, dispatches=len(iv), mean_us=round(sum(d) / len(d) / 1e3, 3),
+                min_us=round(min(d) / 1e3, 3), max_us=round(max(d) / 1e3, 3),
+                union_us_per_dispatch=round(union / len(iv) / 1e3, 3))
 
 
 if __name__ == "__main__":
