@@ -2984,9 +2984,10 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
   if (!r) return set_err(-EINVAL, "handle is NULL");
   const bool tr = repeat_trace_on();
   if (tr) r->trace[0] = now_s();
-  int cur = -1;
-  HIP_TRY(hipGetDevice(&cur));
-  if (cur != r->device) return set_err(-EINVAL, "handle belongs to device %d, thread is on %d", r->device, cur);
+  // (no current-device check here: the handle's streams, events and buffers
+  // all belong to r->device, so its launches go there whatever device the
+  // calling thread has selected -- and hipGetDevice cost ~5 us at the head of
+  // a timed region, profiles/bench_regions_r02.jsonl)
   const bool timed = flags & MI_TIME_REGION;
   const uint32_t ns = r->nstreams;
   if (flags & MI_REPEAT_AFTER_DEFAULT) {  // order after the legacy default stream's queued work
