@@ -131,6 +131,29 @@ __device__ __forceinline__ uint32_t group_lane(uint32_t x, uint32_t k) {
   }
 }
 
+// A DPP move computed by EVERY lane at this point.  A DPP result consumed only
+// under a condition may otherwise be sunk into a branch, where the lanes it
+// reads from are switched off and read back as 0.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_all(uint32_t x) {
+  uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+  asm volatile("" : "+v"(y));
+  return y;
+}
+
+// Inclusive prefix sum inside each G-lane group (DPP, no LDS).
+template <int G>
+__device__ __forceinline__ uint32_t group_scan(uint32_t x) {
+  const uint32_t lg = threadIdx.x & (G - 1);
+  if constexpr (G >= 2) { const uint32_t y = dpp_all<0x111>(x); x += lg >= 1 ? y : 0u; }  // row_shr:1
+  if constexpr (G >= 4) { const uint32_t y = dpp_all<0x112>(x); x += lg >= 2 ? y : 0u; }  // row_shr:2
+  if constexpr (G >= 8) { const uint32_t y = dpp_all<0x114>(x); x += lg >= 4 ? y : 0u; }  // row_shr:4
+  if constexpr (G >= 16) { const uint32_t y = dpp_all<0x118>(x); x += (lg & 15u) >= 8 ? y : 0u; }  // row_shr:8
+  if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  if constexpr (G == 64) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 struct Desc {
   const uint8_t *base;
   uint32_t bytes;  // bounds-check size (rounded up to 16)
@@ -1347,18 +1370,115 @@ __device__ __forceinline__ uint32_t group_fold(__amdgpu_buffer_rsrc_t r, uint32_
   return fold16(group_sum<G>(acc));
 }
 
+// Fast path of k_chain: a chain whose selected bytes fall in at most
+// kChainPieces nonempty mbufs (the socket-buffer and rte_mbuf chains: a header
+// mbuf and 1-2 cluster pieces).  The group loads the chain's (m_data, m_len)
+// one mbuf per lane, finds each mbuf's piece of the selected stream range
+// [lo, hi) by a group scan -- the same pieces the reference's walk visits --
+// and then folds all pieces in ONE chunk-flat pass: chunk c of the
+// concatenation of the pieces' aligned chunk runs, every load of every piece
+// in flight together, instead of a serial walk with a load round trip and a
+// group reduction per mbuf.  A piece the reference byte-swaps ((clen ^ addr)
+// & 1, in_cksum.c:222-225) is credited as x << 8: x * 256 is x swapped modulo
+// 0xffff and zero iff x is, which is all the final fold sees.
+constexpr int kChainPieces = 4;
+
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
+  __shared__ uint32_t s_pc[kBlock / G][kChainPieces][4];  // source offset, length, swap
   Desc d{};
   d.base = cd.base;
   d.bytes = cd.bytes;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
+  const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
   for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < cd.n; i += stride) {
     uint32_t k = cd.pkt_seg[i];
     const uint32_t kend = cd.pkt_seg[i + 1];
     uint64_t sum = 0;
+    // ---- fast path: one mbuf per lane, pieces by a group scan
+    const int64_t lo = cd.skip[i];
+    const int64_t hi = cd.pseudo ? lo + (int64_t)cd.len[i] : (int64_t)cd.len[i];
+    const uint32_t nseg = kend > k ? kend - k : 0u;
+    int32_t ml = 0;
+    uint64_t so = 0;
+    if ((uint32_t)lane < nseg && nseg <= (uint32_t)G) {
+      ml = cd.seg_len[k + lane];
+      so = cd.seg_off[k + lane];
+    }
+    // flat only with non-negative, < 16 MiB mbufs (no u32 wrap in the scan),
+    // offsets the bounds check can take, and (pseudo) off0 inside the first
+    // mbuf, as in_cksum_pseudo_header assumes
+    const bool odd_seg = ml < 0 || ml > 0xffffff || so >= kOOB;
+    bool flat = nseg <= (uint32_t)G && group_lane<G>(group_sum<G>(odd_seg ? 1u : 0u), 0) == 0u && lo >= 0;
+    if (cd.pseudo && flat && nseg) flat = group_lane<G>((uint32_t)ml, 0) >= (uint32_t)lo;
+    if (flat) {
+      const uint32_t l = (uint32_t)ml;
+      const uint32_t inc = group_scan<G>(l);
+      const int64_t pos = (int64_t)(inc - l);
+      const int64_t a = max(pos, lo), e = min(pos + (int64_t)l, hi);
+      const uint32_t nz = e > a ? 1u : 0u;
+      const uint32_t zi = group_scan<G>(nz);
+      const uint32_t m = group_lane<G>(zi, G - 1);
+      if (m <= (uint32_t)kChainPieces) {
+        if (nz) {
+          const uint32_t A = (uint32_t)(so + (uint64_t)(a - pos));
+          const uint32_t clen = (uint32_t)(a - lo);
+          s_pc[grp][zi - 1][0] = A;
+          s_pc[grp][zi - 1][1] = (uint32_t)(e - a);
+          s_pc[grp][zi - 1][2] = (clen ^ (uint32_t)((uintptr_t)cd.base + A)) & 1u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // pieces 0..m-1 as registers (named fields: an indexed array would go to scratch)
+        auto fld = [&](uint32_t e2, int f) { return e2 < m ? s_pc[grp][e2][f] : 0u; };
+        const uint32_t A0 = fld(0, 0), A1 = fld(1, 0), A2 = fld(2, 0), A3 = fld(3, 0);
+        const uint32_t N0 = fld(0, 1), N1 = fld(1, 1), N2 = fld(2, 1), N3 = fld(3, 1);
+        const uint32_t W0 = fld(0, 2), W1 = fld(1, 2), W2 = fld(2, 2), W3 = fld(3, 2);
+        __builtin_amdgcn_wave_barrier();  // s_pc is rewritten by the group's next chain
+        auto nch = [](uint32_t A, uint32_t n) { return n ? ((A & 15u) + n + 15u) >> 4 : 0u; };
+        const uint32_t P1 = nch(A0, N0), P2 = P1 + nch(A1, N1), P3 = P2 + nch(A2, N2), T = P3 + nch(A3, N3);
+        if (cd.pseudo && nseg)
+          sum = (uint64_t)cd.src[i] + cd.dst[i] + ((uint32_t)cd.proto[i] << 8) +
+                swap16((uint32_t)cd.len[i] & 0xffffu);  // in_cksum.c:252-253
+        uint32_t acc = 0;
+        const uint32_t npass = (T + G * U - 1) / (G * U);
+        for (uint32_t p = 0; p < npass; ++p) {
+          u32x4 v[U];
+          uint32_t pc[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t c = p * (G * U) + u * G + lane;
+            const bool j1 = c >= P1, j2 = c >= P2, j3 = c >= P3;
+            const uint32_t A = j3 ? A3 : j2 ? A2 : j1 ? A1 : A0;
+            const uint32_t P = j3 ? P3 : j2 ? P2 : j1 ? P1 : 0u;
+            pc[u] = c;
+            v[u] = ld16(r, c < T ? (A & ~15u) + 16u * (c - P) : kOOB);
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t c = pc[u];
+            const bool j1 = c >= P1, j2 = c >= P2, j3 = c >= P3;
+            const uint32_t A = j3 ? A3 : j2 ? A2 : j1 ? A1 : A0;
+            const uint32_t N = j3 ? N3 : j2 ? N2 : j1 ? N1 : N0;
+            const uint32_t Wp = j3 ? W3 : j2 ? W2 : j1 ? W1 : W0;
+            const uint32_t P = j3 ? P3 : j2 ? P2 : j1 ? P1 : 0u;
+            const int rel = (int)(16u * (c - P)) - (int)(A & 15u);
+            const bool pure = rel >= 0 && rel + 16 <= (int)N;
+            uint32_t x = pure ? sum4(v[u]) : 0u;
+            if (!pure && c < T) x = range_sum(v[u], rel, 0, (int)N);
+            acc += Wp ? x << 8 : x;
+          }
+          acc = fold16(acc);
+        }
+        sum += fold16(group_sum<G>(acc));
+        if (lane == 0) out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+        continue;
+      }
+    }
+    // ---- general walk (long chains, negative m_len, off0 past the first mbuf)
     int64_t clen = 0;
     // fold one piece of the chain: `mlen` bytes at buffer offset `a`
     auto piece = [&](uint64_t a, int64_t mlen) {
@@ -1453,29 +1573,6 @@ struct TxDesc {
   uint64_t dst_stride, dst_first;
   uint8_t *status;
 };
-
-// A DPP move computed by EVERY lane at this point.  A DPP result consumed only
-// under a condition may otherwise be sunk into a branch, where the lanes it
-// reads from are switched off and read back as 0.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_all(uint32_t x) {
-  uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
-  asm volatile("" : "+v"(y));
-  return y;
-}
-
-// Inclusive prefix sum inside each G-lane group (DPP, no LDS).
-template <int G>
-__device__ __forceinline__ uint32_t group_scan(uint32_t x) {
-  const uint32_t lg = threadIdx.x & (G - 1);
-  if constexpr (G >= 2) { const uint32_t y = dpp_all<0x111>(x); x += lg >= 1 ? y : 0u; }  // row_shr:1
-  if constexpr (G >= 4) { const uint32_t y = dpp_all<0x112>(x); x += lg >= 2 ? y : 0u; }  // row_shr:2
-  if constexpr (G >= 8) { const uint32_t y = dpp_all<0x114>(x); x += lg >= 4 ? y : 0u; }  // row_shr:4
-  if constexpr (G >= 16) { const uint32_t y = dpp_all<0x118>(x); x += (lg & 15u) >= 8 ? y : 0u; }  // row_shr:8
-  if constexpr (G >= 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
-  if constexpr (G == 64) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
-  return x;
-}
 
 // The 16 bytes at source address a (any alignment): the aligned chunk at
 // a & ~15 and (unless aligned) the next one, funnel-shifted.

@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -46,10 +47,11 @@ def layouts(dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--only-chain", action="store_true", help="just the scatter-gather chain op")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
-    for name, n, lsum, size, make in layouts(dev):
+    for name, n, lsum, size, make in ([] if args.only_chain else layouts(dev)):
         R = max(2, -(-(1 << 30) // size))
         bufs = [torch.empty(size, dtype=torch.uint8, device=dev) for _ in range(R)]
         for b in bufs:
@@ -116,16 +118,19 @@ def main():
     e1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
     e0.record(streams[0])
     streams[1].wait_event(e0)
+    t_host = time.perf_counter()
     for k in range(args.steps):
         fn(k % R, streams[k % 2])
     for e, s in zip(e1, streams):
         e.record(s)
+    t_host = time.perf_counter() - t_host
     torch.cuda.synchronize()
     us = max(e0.elapsed_time(e) for e in e1) * 1e3 / args.steps
     lsum = int(c["pkt_len"].sum()) - 34 * n
     alg = lsum + 2 * n
     print(json.dumps(dict(layout="socket chains 1514 B", op="chain_batch (in_cksum_skip over mbuf chains)",
                           datagrams=n, segments_per_chain=round(len(c["seg_len"]) / n, 2), us_per_launch=round(us, 2),
+                          host_us_per_call=round(t_host * 1e6 / args.steps, 2), shape=os.environ.get("MI_CKSUM_SHAPE", "auto"),
                           GiBps=round(lsum / (us / 1e6) / 2**30, 1),
                           roofline=dict(bound="hbm", achieved=round(alg / (us / 1e6) / 1e9, 1), peak=PEAK, unit="GB/s",
                                         frac=round(alg / (us / 1e6) / 1e9 / PEAK, 4), alg_bytes_per_launch=int(alg)))),
