@@ -63,9 +63,10 @@ def parse():
     ap.add_argument("--offs64", action="store_true",
                     help="pareto: u64 packet offsets instead of u32 (MI_BATCH_OFFS32, 4 B less per datagram)")
     ap.add_argument("--streams", type=int, default=2, help="streams the steps alternate over")
-    ap.add_argument("--submit", default="launch", choices=["graph", "launch"],
+    ap.add_argument("--submit", default="aql", choices=["graph", "launch", "aql"],
                     help="launch: K host launches from native code; graph: the same K launches as one cached "
-                         "hipGraph (measured slower for 1500 B: profiles/submit_r01.jsonl)")
+                         "hipGraph (measured slower for 1500 B: profiles/submit_r01.jsonl); aql: the same kernels "
+                         "as K prebuilt AQL packets in the handle's own HSA queue (MI_REPEAT_ENGINE_AQL)")
     ap.add_argument("--settle", type=float, default=0.3,
                     help="untimed warm-up lasts at least this many seconds (GPU clock settle)")
     return ap.parse_args()
@@ -161,7 +162,18 @@ def main():
     # non-blocking streams so a launch's ramp-up overlaps its predecessor's drain.
     nst = max(1, args.streams)
     use_graph = args.submit == "graph"
-    rep = None if use_graph else mi.VerifyRepeat(batches, outs, nstreams=nst)
+    # Default: the AQL engine -- the same kernels as prebuilt AQL packets in
+    # the handle's own HSA queues (one per stream), so a 20-step region pays
+    # ~1 us of submission instead of ~50-80 us of HIP launches and its wait
+    # ends ~10 us sooner (profiles/aql_r02.jsonl: 5941-6027 vs 5429-5674 GiB/s
+    # by wall clock, same GPU span per pass).
+    rep, engine_note = None, None
+    if not use_graph:
+        try:
+            rep = mi.VerifyRepeat(batches, outs, nstreams=nst, engine="aql" if args.submit == "aql" else "hip")
+        except mi.MiCksumError as e:  # the same kernels through HIP launches
+            engine_note = f"AQL engine unavailable ({e}); HIP launches"
+            rep = mi.VerifyRepeat(batches, outs, nstreams=nst)
 
     def run(k: int, timed: bool = False):
         if rep is not None:
@@ -184,7 +196,9 @@ def main():
         run(500, timed=True)
         settle_steps += 500
     cfg["settle_steps"] = settle_steps
-    cfg["submit"] = "graph" if use_graph else "prepared handle, host launches"
+    cfg["submit"] = ("graph" if use_graph else engine_note if engine_note else
+                     f"prepared handle, AQL packets ({nst} own HSA queues)" if args.submit == "aql"
+                     else "prepared handle, host launches")
     cfg["wait"] = args.wait
     if use_graph:  # instantiate the timed region's graph (K passes) before timing it
         run(args.steps)

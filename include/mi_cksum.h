@@ -332,6 +332,25 @@ void mi_cksum_repeat_destroy(mi_repeat *r);
 #define MI_REPEAT_OP_VERIFY   0u
 #define MI_REPEAT_OP_FINALIZE 1u
 int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op);
+/* How a run submits its passes.
+ * MI_REPEAT_ENGINE_HIP (default): HIP launches alternating over the handle's
+ *   nstreams streams.
+ * MI_REPEAT_ENGINE_AQL: the kernel arguments and one AQL dispatch packet per
+ *   batch are built once, here; a run copies its passes' packets into the
+ *   handle's own HSA queues, rings the
+ *   doorbell and spins on one completion signal.  Pass k goes to queue
+ *   k % nqueues (nqueues = nstreams, 1..4); each queue runs its passes in
+ *   order and the queues overlap, as the HIP engine's streams do.  Same
+ *   kernels, same results.
+ *   Verify passes of uniform, packed and 64-byte-slot batches (not
+ *   length-class batches: -ENOTSUP).  A run does not order itself after HIP
+ *   streams: complete the batches' producers first (or pass
+ *   MI_REPEAT_AFTER_DEFAULT: a host-side wait on the legacy default stream).
+ *   Results reach L2 and HBM with the packets' system-scope release.
+ * Returns 0, -ENOTSUP / -ENOENT when the engine cannot serve the handle. */
+#define MI_REPEAT_ENGINE_HIP 0u
+#define MI_REPEAT_ENGINE_AQL 1u
+int mi_cksum_repeat_set_engine(mi_repeat *r, uint32_t engine);
 
 /*
  * Completion waits on the calling thread's current device busy-poll (on != 0:

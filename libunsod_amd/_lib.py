@@ -154,6 +154,7 @@ SIGNATURES = {
     "mi_cksum_repeat_destroy": (None, [C.c_void_p]),
     "mi_cksum_set_busy_wait": (C.c_int, [C.c_int]),
     "mi_cksum_repeat_set_op": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "mi_cksum_repeat_set_engine": (C.c_int, [C.c_void_p, C.c_uint32]),
     "mi_cksum_ipv4_verify_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p]),
     "mi_cksum_rx_offload_host": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p]),

@@ -372,9 +372,14 @@ class VerifyRepeat:
     """A prepared back-to-back verify submission (mi_cksum_repeat_*): pass k
     over batches[k % nb] into outs[k % nb], on the k % nstreams-th of the
     handle's own non-blocking streams.  Everything is marshalled once here, so
-    ``run`` costs one ctypes call plus the launches and the wait."""
+    ``run`` costs one ctypes call plus the launches and the wait.
 
-    def __init__(self, batches, outs=None, nstreams: int = 2, op: str = "verify"):
+    ``engine="aql"`` (mi_cksum_repeat_set_engine, MI_REPEAT_ENGINE_AQL): the
+    passes go out as prebuilt AQL packets in the handle's own HSA queue(s)
+    instead of HIP launches (verify only; the batches' producers must have
+    completed -- ``after_default`` waits for the legacy stream on the host)."""
+
+    def __init__(self, batches, outs=None, nstreams: int = 2, op: str = "verify", engine: str = "hip"):
         nb = len(batches)
         self._keep = (batches, outs)
         arr = (PktBatchC * nb)(*[b.c for b in batches])
@@ -389,6 +394,9 @@ class VerifyRepeat:
         if op != "verify":
             check("mi_cksum_repeat_set_op",
                   lib.mi_cksum_repeat_set_op(h, {"finalize": 1}[op]))
+        self.engine = engine
+        if engine != "hip":
+            check("mi_cksum_repeat_set_engine", lib.mi_cksum_repeat_set_engine(h, {"aql": 1}[engine]))
         self._run = lib.mi_cksum_repeat_run
         self._span = C.c_float(0.0)
         self._span_ref = C.byref(self._span)

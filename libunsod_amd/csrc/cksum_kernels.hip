@@ -40,6 +40,12 @@
 #include <string.h>
 #include <time.h>
 
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <hsa/hsa_ven_amd_loader.h>
+
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -643,10 +649,10 @@ __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uin
 }
 
 // RX verify: ip_input.c:459-471 + tcp_input.c:697-720, one pass per datagram.
+// (the body is shared with the AQL engine's extern "C" entry points, mi_aql_*)
 template <int G, int U>
-__global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out,
-                                                        uint16_t *l4_out, uint8_t *st_out,
-                                                        uint32_t *bad) {
+__device__ __forceinline__ void verify_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                            uint32_t *bad) {
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
   VOut pend;  // the previous datagram's outputs, emitted once this one's loads are in flight
@@ -665,6 +671,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
     }
   });
   if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+}
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                                        uint32_t *bad) {
+  verify_body<G, U>(d, ip_out, l4_out, st_out, bad);
 }
 
 // RX verify of SEVERAL batches in one launch (mi_cksum_ipv4_verify_multi): a
@@ -907,10 +918,8 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 // MODE: 0 RX verify; 1 TX finalize in place (finalize_store); 2 span folds
 // (mi_cksum_span_batch: out = ip_out, in_cksum_skip / pseudo-header seeds).
 template <int U, int MODE = 0>
-__global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
-                                                               uint16_t *l4_out, uint8_t *st_out,
-                                                               uint32_t *bad, SpanSeeds sp,
-                                                               uint32_t abs_lanes) {
+__device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                            uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes) {
   constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[kBlock / 64][W];
@@ -1104,6 +1113,11 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
     verify_emit(pend, ip_out, l4_out, st_out, bad, d);
   }
 }
+template <int U, int MODE = 0>
+__global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                                   uint32_t *bad, SpanSeeds sp, uint32_t abs_lanes) {
+  packed_body<U, MODE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+}
 
 // RX verify of minimum-size frames in 64-byte slots (stride 64, the datagram
 // inside its slot, starting < 16 bytes in: the 64 B config, 46 B datagrams at
@@ -1112,8 +1126,8 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out,
 // hands lane k its own slot's four chunks, and the lane folds its datagram
 // directly -- no scan, no per-datagram header / tail reloads (which cost the
 // flat-run kernel four scattered 16-byte L2 requests per datagram).
-__global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t *ip_out, uint16_t *l4_out,
-                                                               uint8_t *st_out, uint32_t *bad) {
+__device__ __forceinline__ void slot64_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                            uint32_t *bad) {
   __shared__ u32x4 s_slot[kBlock / 64][256];
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -1164,6 +1178,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
     }
   }
   verify_emit(pend, ip_out, l4_out, st_out, bad, d);
+}
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                               uint8_t *st_out, uint32_t *bad) {
+  slot64_body(d, ip_out, l4_out, st_out, bad);
 }
 
 // TX finalize in place: in_delayed_cksum (ip_output.c:958-983) + ip_sum
@@ -2177,6 +2195,34 @@ __global__ __launch_bounds__(kScalarThreads) void k_scalar(const uint8_t *base, 
   }
 }
 
+}  // namespace
+
+// AQL entry points (the repeat handle's AQL engine, MI_REPEAT_ENGINE_AQL): the
+// RX verify kernels again, under extern "C" names, so the engine can find their
+// kernel descriptors by name in the code object HIP loaded and dispatch them
+// with packets it writes itself.  One argument list for all of them.
+#define MI_AQL_SHAPE(G_, U_)                                                                            \
+  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_v_##G_##x##U_(                           \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
+    verify_body<G_, U_>(d, ip, l4, st, bad);                                                            \
+  }
+#define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12)
+MI_AQL_SHAPES(MI_AQL_SHAPE)
+#define MI_AQL_RUN(U_)                                                                                  \
+  extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
+                                                           uint32_t *bad) {                             \
+    packed_body<U_, 0>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                                            \
+  }
+MI_AQL_RUN(4)
+MI_AQL_RUN(8)
+MI_AQL_RUN(16)
+extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st,
+                                                                   uint32_t *bad) {
+  slot64_body(d, ip, l4, st, bad);
+}
+
+namespace {
+
 // ------------------------------------------------------------------- runtime
 thread_local char t_err[256];
 
@@ -2483,19 +2529,30 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
   return {kPlanClasses, {0, 0}, 0};
 }
 
+// Grids of the flat-run and 64-byte-slot kernels: 64 datagrams per wave.
+unsigned run_blocks(const Desc &d) {
+  static const int run_cap = [] {
+    const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 16384;
+  }();
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap;
+  uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+  if (blocks > (uint64_t)cap) blocks = cap;
+  return blocks ? (unsigned)blocks : 1u;
+}
+unsigned slot64_blocks(const Desc &d) {
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+  uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+  if (blocks > (uint64_t)cap) blocks = cap;
+  return blocks ? (unsigned)blocks : 1u;
+}
+
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
   const Plan pl = verify_plan(d, max_len);
   if (pl.kind == kPlanRun) {
-    static const int run_cap = [] {
-      const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
-      const int v = e ? atoi(e) : 0;
-      return v > 0 ? v : 16384;
-    }();
-    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap;
-    uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 datagrams per wave
-    if (blocks > (uint64_t)cap) blocks = cap;
-    const dim3 grid(blocks ? (unsigned)blocks : 1u);
+    const dim3 grid(run_blocks(d));
     if (pl.run_u == 4)
       VLAUNCH((k_ipv4_verify_packed<4>), grid, dim3(kBlock), 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
     else if (pl.run_u == 16)
@@ -2505,10 +2562,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     return launched();
   }
   if (pl.kind == kPlanSlot64) {
-    const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
-    uint64_t blocks = ((uint64_t)d.n + 255) / 256;  // 64 slots per wave
-    if (blocks > (uint64_t)cap) blocks = cap;
-    VLAUNCH(k_ipv4_verify_slot64, dim3(blocks ? (unsigned)blocks : 1u), dim3(kBlock), 0, s, d, ip, l4, st, bad);
+    VLAUNCH(k_ipv4_verify_slot64, dim3(slot64_blocks(d)), dim3(kBlock), 0, s, d, ip, l4, st, bad);
     return launched();
   }
   if (pl.kind == kPlanShape) return launch_verify_shape(d, pl.shape, ip, l4, st, bad, s);
@@ -2627,6 +2681,414 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
   FOR_TX_GU(X)
 #undef X
   return set_err(-EINVAL, "no TX kernel for shape %dx%d", sh.g, sh.u);
+}
+
+// ---------------------------------------------------------------- AQL engine
+// The repeat handle's second submission engine (MI_REPEAT_ENGINE_AQL).  An RX
+// queue loop re-submits the same few batches forever, so everything about a
+// pass -- kernel descriptor, grid, the kernel arguments (device-resident,
+// written once), the dispatch packet itself -- is fixed at set-up; a run only
+// copies K prebuilt 64-byte AQL packets into a private HSA queue, rings its
+// doorbell and spins on one completion signal.  Consecutive packets carry no
+// barrier bit, so the packet processor starts pass k+1 as soon as pass k has
+// dispatched its last workgroup (the overlap the HIP engine needs two streams
+// for).  What a HIP launch adds per call (runtime bookkeeping, per-launch
+// kernel-argument staging, marker packets for events, completion processing)
+// is gone; the GPU work is identical -- the same kernel bodies (mi_aql_*).
+enum AqlKernelId {
+#define X(G_, U_) kAqlV_##G_##x##U_,
+  MI_AQL_SHAPES(X)
+#undef X
+  kAqlRun4, kAqlRun8, kAqlRun16, kAqlSlot64, kAqlKernels
+};
+const char *const kAqlNames[kAqlKernels] = {
+#define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
+    MI_AQL_SHAPES(X)
+#undef X
+    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_slot64"};
+const void *const kAqlFuncs[kAqlKernels] = {
+#define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
+    MI_AQL_SHAPES(X)
+#undef X
+    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_slot64};
+
+// The kernels' explicit arguments, laid out as the compiler lays out the
+// kernel-argument segment (each parameter at its natural alignment).  The
+// code object v5 hidden arguments follow at the next 8-byte boundary.
+struct AqlArgs {
+  Desc d;
+  uint16_t *ip, *l4;
+  uint8_t *st;
+  uint32_t *bad;
+};
+constexpr uint32_t kAqlHidden = (sizeof(AqlArgs) + 7u) & ~7u;
+
+struct AqlKernel {
+  uint64_t object = 0;
+  uint32_t kernarg = 0, group = 0, priv = 0;
+};
+struct AqlDevice {
+  bool tried = false;
+  int rc = 0;
+  char err[160] = {};
+  hsa_agent_t agent{};
+  double ns_per_tick = 1.0;
+  AqlKernel k[kAqlKernels];
+};
+std::mutex g_aql_mu;
+AqlDevice g_aql[64];
+std::atomic<int> g_aql_queue_error{0};
+
+struct AqlFind {
+  hsa_agent_t agent;
+  AqlKernel *k;
+  int found;
+};
+hsa_status_t aql_symbol_cb(hsa_executable_t, hsa_agent_t, hsa_executable_symbol_t sym, void *data) {
+  AqlFind *f = (AqlFind *)data;
+  hsa_symbol_kind_t kind;
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_TYPE, &kind) != HSA_STATUS_SUCCESS ||
+      kind != HSA_SYMBOL_KIND_KERNEL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t len = 0;
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME_LENGTH, &len) != HSA_STATUS_SUCCESS ||
+      len == 0 || len > 200)
+    return HSA_STATUS_SUCCESS;
+  char name[208] = {};
+  if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_NAME, name) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  name[len] = 0;
+  if (len > 3 && !strcmp(name + len - 3, ".kd")) name[len - 3] = 0;
+  for (int i = 0; i < kAqlKernels; ++i) {
+    if (strcmp(name, kAqlNames[i]) || f->k[i].object) continue;
+    AqlKernel &k = f->k[i];
+    if (hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_OBJECT, &k.object) ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_KERNARG_SEGMENT_SIZE, &k.kernarg) ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_GROUP_SEGMENT_SIZE, &k.group) ||
+        hsa_executable_symbol_get_info(sym, HSA_EXECUTABLE_SYMBOL_INFO_KERNEL_PRIVATE_SEGMENT_SIZE, &k.priv)) {
+      k = AqlKernel();
+      continue;
+    }
+    ++f->found;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t aql_exe_cb(hsa_executable_t exe, void *data) {
+  AqlFind *f = (AqlFind *)data;
+  (void)hsa_executable_iterate_agent_symbols(exe, f->agent, aql_symbol_cb, data);
+  return HSA_STATUS_SUCCESS;
+}
+struct AqlAgentFind {
+  uint32_t bdf, domain;
+  hsa_agent_t agent;
+  bool found;
+};
+hsa_status_t aql_agent_cb(hsa_agent_t a, void *data) {
+  AqlAgentFind *f = (AqlAgentFind *)data;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) != HSA_STATUS_SUCCESS ||
+      hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) != HSA_STATUS_SUCCESS)
+    return HSA_STATUS_SUCCESS;
+  if (bdf == f->bdf && dom == f->domain) {
+    f->agent = a;
+    f->found = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+// The HSA agent behind a HIP device and the mi_aql_* kernel descriptors in the
+// code object HIP loaded for it (resolved once per device).
+int aql_device(int dev, AqlDevice **out) {
+  if (dev < 0 || dev >= 64) return set_err(-EINVAL, "device %d", dev);
+  std::lock_guard<std::mutex> lk(g_aql_mu);
+  AqlDevice &a = g_aql[dev];
+  if (!a.tried) {
+    a.tried = true;
+#define fail(code, ...)                    \
+  do {                                     \
+    snprintf(a.err, sizeof a.err, __VA_ARGS__); \
+    a.rc = (code);                         \
+  } while (0)
+    // HIP may load a code object lazily: querying the kernels loads it
+    for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
+      hipFuncAttributes fa;
+      if (hipFuncGetAttributes(&fa, kAqlFuncs[i]) != hipSuccess) fail(-EIO, "hipFuncGetAttributes(%s)", kAqlNames[i]);
+    }
+    hipDeviceProp_t prop;
+    if (!a.rc && hipGetDeviceProperties(&prop, dev) != hipSuccess) fail(-EIO, "hipGetDeviceProperties");
+    if (!a.rc && hsa_init() != HSA_STATUS_SUCCESS) fail(-EIO, "hsa_init");
+    AqlAgentFind af{(uint32_t)((prop.pciBusID << 8) | (prop.pciDeviceID << 3)), (uint32_t)prop.pciDomainID, {}, false};
+    if (!a.rc) {
+      (void)hsa_iterate_agents(aql_agent_cb, &af);
+      if (!af.found) fail(-ENODEV, "no HSA agent at PCI %04x:%02x:%02x", af.domain, prop.pciBusID, prop.pciDeviceID);
+    }
+    if (!a.rc) {
+      a.agent = af.agent;
+      uint64_t freq = 0;
+      if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &freq) == HSA_STATUS_SUCCESS && freq)
+        a.ns_per_tick = 1e9 / (double)freq;
+      AqlFind f{a.agent, a.k, 0};
+      hsa_ven_amd_loader_1_03_pfn_t ldr{};
+      if (hsa_system_get_major_extension_table(HSA_EXTENSION_AMD_LOADER, 1, sizeof ldr, &ldr) != HSA_STATUS_SUCCESS ||
+          !ldr.hsa_ven_amd_loader_iterate_executables)
+        fail(-ENOTSUP, "no HSA loader extension 1.03");
+      else
+        (void)ldr.hsa_ven_amd_loader_iterate_executables(aql_exe_cb, &f);
+      for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
+        if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
+        else if (a.k[i].kernarg < kAqlHidden || a.k[i].kernarg > 1024u)
+          fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
+               (unsigned)sizeof(AqlArgs));
+      }
+    }
+  }
+#undef fail
+  if (a.rc) return set_err(a.rc, "AQL engine: %s", a.err);
+  *out = &a;
+  return 0;
+}
+
+// Which mi_aql_* kernel and grid a verify pass over d gets (launch_verify's
+// plan; length-class plans need several launches per pass: not offered).
+int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
+  const Plan pl = verify_plan(d, max_len);
+  if (pl.kind == kPlanRun) {
+    *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
+    *blocks = run_blocks(d);
+    return 0;
+  }
+  if (pl.kind == kPlanSlot64) {
+    *id = kAqlSlot64;
+    *blocks = slot64_blocks(d);
+    return 0;
+  }
+  if (pl.kind == kPlanShape) {
+#define X(G_, U_)                                      \
+  if (pl.shape.g == G_ && pl.shape.u == U_) {          \
+    *id = kAqlV_##G_##x##U_;                           \
+    *blocks = (unsigned)grid_for(d.n, G_);             \
+    return 0;                                          \
+  }
+    MI_AQL_SHAPES(X)
+#undef X
+    return set_err(-ENOTSUP, "AQL engine: no entry point for shape %dx%d", pl.shape.g, pl.shape.u);
+  }
+  return set_err(-ENOTSUP, "AQL engine: length-class batches take several launches per pass");
+}
+
+void aql_queue_error(hsa_status_t st, hsa_queue_t *, void *) { g_aql_queue_error.store((int)st); }
+
+// Fence scopes of the dispatch packets (MI_CKSUM_AQL_RELEASE=agent: release at
+// agent scope -- results stay in L2 for later kernels, not for DMA engines).
+uint16_t aql_release_scope() {
+  static const uint16_t sc = [] {
+    const char *e = getenv("MI_CKSUM_AQL_RELEASE");
+    return (uint16_t)(e && !strcmp(e, "agent") ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM);
+  }();
+  return sc;
+}
+
+// Barrier bit of every packet (MI_CKSUM_AQL_BARRIER, default 1): each queue
+// runs its passes in order, like a HIP stream, and consecutive passes overlap
+// across queues.  With 0 a queue may start pass k+1 once pass k has dispatched
+// its last workgroup; measured on MI355X that overlaps little within one
+// queue (1500 B: 17.9 us per pass on one queue vs 15.0-15.2 on two,
+// profiles/aql_r02.jsonl).
+uint32_t aql_barrier() {
+  static const uint32_t b = [] {
+    const char *e = getenv("MI_CKSUM_AQL_BARRIER");
+    return e && e[0] == '0' ? 0u : 1u;
+  }();
+  return b;
+}
+
+struct AqlRun {
+  AqlDevice *dev = nullptr;
+  uint32_t nq = 1;
+  hsa_queue_t *q[4] = {};
+  hsa_signal_t first{}, rest{};  // pass 0's completion (timing start) / every other pass's
+  bool have_first = false, have_rest = false;
+  uint8_t *kargs = nullptr;      // device memory: one argument block per batch
+  std::vector<hsa_kernel_dispatch_packet_t> pkt;  // one prebuilt packet per batch
+  uint32_t last_steps = 0;
+  bool pending = false;
+};
+
+void aql_free(AqlRun *a) {
+  if (!a) return;
+  for (auto *q : a->q)
+    if (q) (void)hsa_queue_destroy(q);
+  if (a->have_first) (void)hsa_signal_destroy(a->first);
+  if (a->have_rest) (void)hsa_signal_destroy(a->rest);
+  if (a->kargs) (void)hipFree(a->kargs);
+  delete a;
+}
+
+// Build the engine for nb batches: kernel-argument blocks (device memory,
+// written once) and one dispatch packet template per batch.
+int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *const *ip, uint16_t *const *l4,
+               uint8_t *const *st, uint32_t nb, uint32_t nqueues, AqlRun **out) {
+  AqlDevice *dv = nullptr;
+  int rc = aql_device(device, &dv);
+  if (rc) return rc;
+  AqlRun *a = new AqlRun();
+  a->dev = dv;
+  a->nq = std::min(std::max(nqueues, 1u), 4u);
+  uint32_t slot = 0;
+  std::vector<int> ids(nb);
+  std::vector<unsigned> blocks(nb);
+  for (uint32_t j = 0; j < nb; ++j) {
+    if ((rc = aql_kernel_for(d[j], max_len[j], &ids[j], &blocks[j]))) {
+      aql_free(a);
+      return rc;
+    }
+    slot = std::max(slot, (dv->k[ids[j]].kernarg + 63u) & ~63u);
+  }
+  std::vector<uint8_t> host((size_t)slot * nb, 0);
+  a->pkt.resize(nb);
+  hipError_t e = hipMalloc((void **)&a->kargs, host.size());
+  if (e != hipSuccess) {
+    aql_free(a);
+    return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
+  }
+  for (uint32_t j = 0; j < nb; ++j) {
+    uint8_t *ka = host.data() + (size_t)slot * j;
+    const AqlArgs args{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr};
+    memcpy(ka, &args, sizeof args);
+    // code object v5 hidden arguments the kernels read: block counts, group
+    // sizes, remainders, grid dimensions (AMDGPUUsage, "hidden_*" offsets)
+    uint8_t *h = ka + kAqlHidden;
+    const uint32_t bc[3] = {blocks[j], 1u, 1u};
+    const uint16_t gs[3] = {(uint16_t)kBlock, 1u, 1u}, rem[3] = {0, 0, 0}, dims = 1;
+    memcpy(h + 0, bc, sizeof bc);
+    memcpy(h + 12, gs, sizeof gs);
+    memcpy(h + 18, rem, sizeof rem);
+    memcpy(h + 64, &dims, sizeof dims);
+    const AqlKernel &k = dv->k[ids[j]];
+    hsa_kernel_dispatch_packet_t &p = a->pkt[j];
+    memset(&p, 0, sizeof p);
+    p.setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+    p.workgroup_size_x = (uint16_t)kBlock;
+    p.workgroup_size_y = 1;
+    p.workgroup_size_z = 1;
+    p.grid_size_x = blocks[j] * (uint32_t)kBlock;
+    p.grid_size_y = 1;
+    p.grid_size_z = 1;
+    p.private_segment_size = k.priv;
+    p.group_segment_size = k.group;
+    p.kernel_object = k.object;
+    p.kernarg_address = a->kargs + (size_t)slot * j;
+  }
+  e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    aql_free(a);
+    return set_err(-EIO, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
+  }
+  for (uint32_t q = 0; q < a->nq; ++q) {
+    if (hsa_queue_create(dv->agent, 4096, HSA_QUEUE_TYPE_SINGLE, aql_queue_error, nullptr, UINT32_MAX, UINT32_MAX,
+                         &a->q[q]) != HSA_STATUS_SUCCESS) {
+      a->q[q] = nullptr;
+      aql_free(a);
+      return set_err(-EIO, "AQL engine: hsa_queue_create failed");
+    }
+    (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
+  }
+  if (hsa_signal_create(0, 0, nullptr, &a->first) != HSA_STATUS_SUCCESS) {
+    aql_free(a);
+    return set_err(-EIO, "AQL engine: hsa_signal_create failed");
+  }
+  a->have_first = true;
+  if (hsa_signal_create(0, 0, nullptr, &a->rest) != HSA_STATUS_SUCCESS) {
+    aql_free(a);
+    return set_err(-EIO, "AQL engine: hsa_signal_create failed");
+  }
+  a->have_rest = true;
+  *out = a;
+  return 0;
+}
+
+// Wait for every pass of the last submission (spinning: the RX loop polls).
+int aql_wait(AqlRun *a) {
+  if (!a->pending) return 0;
+  timespec ts0, ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
+  for (hsa_signal_t s : {a->first, a->rest}) {
+    for (;;) {
+      const hsa_signal_value_t v =
+          hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE);
+      if (v == 0) break;
+      if (g_aql_queue_error.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", g_aql_queue_error.load());
+      clock_gettime(CLOCK_MONOTONIC, &ts);
+      if (ts.tv_sec - ts0.tv_sec > 10) return set_err(-ETIMEDOUT, "AQL engine: passes not complete after 10 s");
+    }
+  }
+  a->pending = false;
+  return 0;
+}
+
+// Submit `steps` passes starting with batch j0.
+int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
+  if (!steps) return 0;
+  const uint32_t nb = (uint32_t)a->pkt.size();
+  hsa_signal_store_relaxed(a->first, 1);
+  hsa_signal_store_relaxed(a->rest, (hsa_signal_value_t)(steps - 1));
+  const uint16_t rel = aql_release_scope();
+  const uint32_t hdr_base = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                            (aql_barrier() << HSA_PACKET_HEADER_BARRIER) |
+                            (rel << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+  uint64_t last_idx[4] = {0, 0, 0, 0};
+  bool rung[4] = {false, false, false, false};
+  uint32_t j = j0;
+  for (uint32_t k = 0; k < steps; ++k) {
+    hsa_queue_t *q = a->q[k % a->nq];
+    const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
+    while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+      if (g_aql_queue_error.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", g_aql_queue_error.load());
+    }
+    hsa_kernel_dispatch_packet_t *slot =
+        (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
+    const hsa_kernel_dispatch_packet_t &t = a->pkt[j];
+    // everything but the first 32 bits (header + setup), which go last
+    memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
+    slot->completion_signal = k == 0 ? a->first : a->rest;
+    // the first pass acquires at system scope (the batches' producers), the
+    // rest at agent scope
+    const uint32_t acq = k == 0 ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const uint32_t hs = (hdr_base | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE)) | ((uint32_t)t.setup << 16);
+    __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
+    last_idx[k % a->nq] = idx;
+    if (k < a->nq) {  // start the GPU at once; the rest follow behind one more doorbell
+      hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+      rung[k % a->nq] = true;
+    }
+    j = j + 1 == nb ? 0 : j + 1;
+  }
+  for (uint32_t q = 0; q < a->nq && q < steps; ++q)
+    if (rung[q]) hsa_signal_store_screlease(a->q[q]->doorbell_signal, (hsa_signal_value_t)last_idx[q]);
+  a->last_steps = steps;
+  a->pending = true;
+  return 0;
+}
+
+// GPU span of the last (completed) submission, in us: pass 0's start to the
+// latest completion.
+int aql_span(AqlRun *a, float *span_us) {
+  if (!a->last_steps) return set_err(-EINVAL, "AQL engine: nothing submitted");
+  hsa_amd_profiling_dispatch_time_t t0{}, t1{};
+  if (hsa_amd_profiling_get_dispatch_time(a->dev->agent, a->first, &t0) != HSA_STATUS_SUCCESS)
+    return set_err(-EIO, "AQL engine: dispatch time");
+  uint64_t end = t0.end;
+  if (a->last_steps > 1) {
+    if (hsa_amd_profiling_get_dispatch_time(a->dev->agent, a->rest, &t1) != HSA_STATUS_SUCCESS)
+      return set_err(-EIO, "AQL engine: dispatch time");
+    end = std::max(end, t1.end);
+  }
+  *span_us = (float)((double)(end - t0.start) * a->dev->ns_per_tick * 1e-3);
+  return 0;
 }
 
 }  // namespace
@@ -2974,6 +3436,7 @@ struct mi_repeat {
   uint32_t *flag = nullptr, *flag_dev = nullptr;
   uint32_t seq = 0;
   double trace[8] = {};  // MI_CKSUM_REPEAT_TRACE: host timestamps of the last run (s)
+  AqlRun *aql = nullptr;  // MI_REPEAT_ENGINE_AQL
 };
 
 namespace {
@@ -2987,6 +3450,10 @@ void repeat_free(mi_repeat *r) {
   }
   if (r->ev0) (void)hipEventDestroy(r->ev0);
   if (r->flag) (void)hipHostFree(r->flag);
+  if (r->aql) {
+    (void)aql_wait(r->aql);
+    aql_free(r->aql);
+  }
   delete r;
 }
 
@@ -3081,6 +3548,21 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
   if (!r) return set_err(-EINVAL, "handle is NULL");
   const bool tr = repeat_trace_on();
   if (tr) r->trace[0] = now_s();
+  if (r->aql) {
+    // AQL engine: the passes are packets in the handle's own HSA queue(s)
+    int rc = aql_wait(r->aql);  // a previous asynchronous run
+    if (rc) return rc;
+    if (flags & MI_REPEAT_AFTER_DEFAULT) HIP_TRY(hipStreamSynchronize(nullptr));
+    if (tr) r->trace[1] = r->trace[2] = now_s();
+    if ((rc = aql_submit(r->aql, r->next, steps))) return rc;
+    r->next = (uint32_t)((r->next + (uint64_t)steps) % r->nb);
+    if (tr) r->trace[3] = r->trace[4] = now_s();
+    if (flags & MI_REPEAT_ASYNC) return 0;
+    if ((rc = aql_wait(r->aql))) return rc;
+    if (tr) r->trace[5] = now_s();
+    if ((flags & MI_TIME_REGION) && span_us) return aql_span(r->aql, span_us);
+    return 0;
+  }
   // (no current-device check here: the handle's streams, events and buffers
   // all belong to r->device, so its launches go there whatever device the
   // calling thread has selected -- and hipGetDevice cost ~5 us at the head of
@@ -3174,6 +3656,10 @@ int mi__repeat_trace(mi_repeat *r, double *t, int n) {
 
 int mi_cksum_repeat_span(mi_repeat *r, float *span_us) {
   if (!r || !span_us) return set_err(-EINVAL, "NULL argument");
+  if (r->aql) {
+    const int rc = aql_wait(r->aql);
+    return rc ? rc : aql_span(r->aql, span_us);
+  }
   float span = 0.f;
   for (uint32_t q = 0; q < r->nstreams; ++q) {
     HIP_TRY(hipEventSynchronize(r->ev_end[q]));
@@ -3187,9 +3673,26 @@ int mi_cksum_repeat_span(mi_repeat *r, float *span_us) {
 
 void mi_cksum_repeat_destroy(mi_repeat *r) { repeat_free(r); }
 
+int mi_cksum_repeat_set_engine(mi_repeat *r, uint32_t engine) {
+  if (!r) return set_err(-EINVAL, "handle is NULL");
+  if (engine != MI_REPEAT_ENGINE_HIP && engine != MI_REPEAT_ENGINE_AQL) return set_err(-EINVAL, "engine %u", engine);
+  if (r->aql) {
+    int rc = aql_wait(r->aql);
+    if (rc) return rc;
+    aql_free(r->aql);
+    r->aql = nullptr;
+  }
+  if (engine == MI_REPEAT_ENGINE_HIP) return 0;
+  if (r->op != MI_REPEAT_OP_VERIFY) return set_err(-ENOTSUP, "AQL engine: verify passes only");
+  for (uint32_t q = 0; q < r->nstreams; ++q) HIP_TRY(hipStreamSynchronize(r->s[q]));
+  return aql_create(r->device, r->d.data(), r->ml.data(), r->ip.data(), r->l4.data(), r->st.data(), r->nb,
+                    r->nstreams, &r->aql);
+}
+
 int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op) {
   if (!r) return set_err(-EINVAL, "handle is NULL");
   if (op != MI_REPEAT_OP_VERIFY && op != MI_REPEAT_OP_FINALIZE) return set_err(-EINVAL, "op %u", op);
+  if (r->aql && op != MI_REPEAT_OP_VERIFY) return set_err(-ENOTSUP, "AQL engine: verify passes only");
   r->op = op;
   return 0;
 }
