@@ -2206,7 +2206,7 @@ __global__ __launch_bounds__(kScalarThreads) void k_scalar(const uint8_t *base, 
       Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
     verify_body<G_, U_>(d, ip, l4, st, bad);                                                            \
   }
-#define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12)
+#define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12) X(64, 4)
 MI_AQL_SHAPES(MI_AQL_SHAPE)
 #define MI_AQL_RUN(U_)                                                                                  \
   extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
@@ -2852,6 +2852,18 @@ int aql_device(int dev, AqlDevice **out) {
   return 0;
 }
 
+int aql_kernel_for_shape(const Desc &d, Shape sh, int *id, unsigned *blocks) {
+#define X(G_, U_)                                      \
+  if (sh.g == G_ && sh.u == U_) {                      \
+    *id = kAqlV_##G_##x##U_;                           \
+    *blocks = (unsigned)grid_for(d.n, G_);             \
+    return 0;                                          \
+  }
+  MI_AQL_SHAPES(X)
+#undef X
+  return set_err(-ENOTSUP, "AQL engine: no entry point for shape %dx%d", sh.g, sh.u);
+}
+
 // Which mi_aql_* kernel and grid a verify pass over d gets (launch_verify's
 // plan; length-class plans need several launches per pass: not offered).
 int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
@@ -2866,17 +2878,7 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
     *blocks = slot64_blocks(d);
     return 0;
   }
-  if (pl.kind == kPlanShape) {
-#define X(G_, U_)                                      \
-  if (pl.shape.g == G_ && pl.shape.u == U_) {          \
-    *id = kAqlV_##G_##x##U_;                           \
-    *blocks = (unsigned)grid_for(d.n, G_);             \
-    return 0;                                          \
-  }
-    MI_AQL_SHAPES(X)
-#undef X
-    return set_err(-ENOTSUP, "AQL engine: no entry point for shape %dx%d", pl.shape.g, pl.shape.u);
-  }
+  if (pl.kind == kPlanShape) return aql_kernel_for_shape(d, pl.shape, id, blocks);
   return set_err(-ENOTSUP, "AQL engine: length-class batches take several launches per pass");
 }
 
@@ -2928,6 +2930,37 @@ void aql_free(AqlRun *a) {
   delete a;
 }
 
+// One kernel-argument block: the explicit arguments, then the code object v5
+// hidden arguments the kernels read -- block counts, group sizes, remainders,
+// grid dimensions (AMDGPUUsage "hidden_*"; offsets checked against the
+// kernels' metadata: hidden_block_count_x at 112 = kAqlHidden, _group_size_x
+// +12, _remainder_x +18, _grid_dims +64).  The rest of the block is zero.
+void aql_fill_args(uint8_t *ka, const AqlArgs &args, unsigned blocks) {
+  memcpy(ka, &args, sizeof args);
+  uint8_t *h = ka + kAqlHidden;
+  const uint32_t bc[3] = {blocks, 1u, 1u};
+  const uint16_t gs[3] = {(uint16_t)kBlock, 1u, 1u}, rem[3] = {0, 0, 0}, dims = 1;
+  memcpy(h + 0, bc, sizeof bc);
+  memcpy(h + 12, gs, sizeof gs);
+  memcpy(h + 18, rem, sizeof rem);
+  memcpy(h + 64, &dims, sizeof dims);
+}
+// A dispatch packet without its header (written last, at submission).
+void aql_fill_packet(hsa_kernel_dispatch_packet_t &p, const AqlKernel &k, unsigned blocks, void *kargs) {
+  memset(&p, 0, sizeof p);
+  p.setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
+  p.workgroup_size_x = (uint16_t)kBlock;
+  p.workgroup_size_y = 1;
+  p.workgroup_size_z = 1;
+  p.grid_size_x = blocks * (uint32_t)kBlock;
+  p.grid_size_y = 1;
+  p.grid_size_z = 1;
+  p.private_segment_size = k.priv;
+  p.group_segment_size = k.group;
+  p.kernel_object = k.object;
+  p.kernarg_address = kargs;
+}
+
 // Build the engine for nb batches: kernel-argument blocks (device memory,
 // written once) and one dispatch packet template per batch.
 int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *const *ip, uint16_t *const *l4,
@@ -2956,32 +2989,9 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
   }
   for (uint32_t j = 0; j < nb; ++j) {
-    uint8_t *ka = host.data() + (size_t)slot * j;
-    const AqlArgs args{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr};
-    memcpy(ka, &args, sizeof args);
-    // code object v5 hidden arguments the kernels read: block counts, group
-    // sizes, remainders, grid dimensions (AMDGPUUsage, "hidden_*" offsets)
-    uint8_t *h = ka + kAqlHidden;
-    const uint32_t bc[3] = {blocks[j], 1u, 1u};
-    const uint16_t gs[3] = {(uint16_t)kBlock, 1u, 1u}, rem[3] = {0, 0, 0}, dims = 1;
-    memcpy(h + 0, bc, sizeof bc);
-    memcpy(h + 12, gs, sizeof gs);
-    memcpy(h + 18, rem, sizeof rem);
-    memcpy(h + 64, &dims, sizeof dims);
-    const AqlKernel &k = dv->k[ids[j]];
-    hsa_kernel_dispatch_packet_t &p = a->pkt[j];
-    memset(&p, 0, sizeof p);
-    p.setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-    p.workgroup_size_x = (uint16_t)kBlock;
-    p.workgroup_size_y = 1;
-    p.workgroup_size_z = 1;
-    p.grid_size_x = blocks[j] * (uint32_t)kBlock;
-    p.grid_size_y = 1;
-    p.grid_size_z = 1;
-    p.private_segment_size = k.priv;
-    p.group_segment_size = k.group;
-    p.kernel_object = k.object;
-    p.kernarg_address = a->kargs + (size_t)slot * j;
+    aql_fill_args(host.data() + (size_t)slot * j,
+                  AqlArgs{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr}, blocks[j]);
+    aql_fill_packet(a->pkt[j], dv->k[ids[j]], blocks[j], a->kargs + (size_t)slot * j);
   }
   e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -3088,6 +3098,78 @@ int aql_span(AqlRun *a, float *span_us) {
     end = std::max(end, t1.end);
   }
   *span_us = (float)((double)(end - t0.start) * a->dev->ns_per_tick * 1e-3);
+  return 0;
+}
+
+// One synchronous dispatch per call (the host-memory burst path): a per-thread
+// HSA queue, kernel arguments written into page-locked host memory per call
+// (the burst's descriptors change every time), acquire and release at system
+// scope (the burst and the outputs live in host memory), a spin on the
+// completion signal.  Replaces a HIP launch + hipStreamSynchronize.
+struct AqlOne {
+  int device = -1;
+  AqlDevice *dev = nullptr;
+  hsa_queue_t *q = nullptr;
+  hsa_signal_t sig{};
+  uint8_t *karg = nullptr;  // page-locked, mapped: kAqlOneSlots blocks of 512 B
+  uint32_t next = 0;
+};
+constexpr uint32_t kAqlOneSlots = 8;
+thread_local AqlOne t_aql1;
+
+void aql_one_release(AqlOne &o) {
+  if (o.q) (void)hsa_queue_destroy(o.q);
+  if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
+  if (o.karg) (void)hipHostFree(o.karg);
+  o = AqlOne();
+}
+
+int aql_one_dispatch(int id, unsigned blocks, const AqlArgs &args) {
+  AqlOne &o = t_aql1;
+  if (o.device != t_ctx.device) {
+    aql_one_release(o);
+    int rc = aql_device(t_ctx.device, &o.dev);
+    if (rc) return rc;
+    if (hsa_queue_create(o.dev->agent, 64, HSA_QUEUE_TYPE_SINGLE, aql_queue_error, nullptr, UINT32_MAX, UINT32_MAX,
+                         &o.q) != HSA_STATUS_SUCCESS) {
+      o.q = nullptr;
+      return set_err(-EIO, "AQL engine: hsa_queue_create failed");
+    }
+    if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
+      aql_one_release(o);
+      return set_err(-EIO, "AQL engine: hsa_signal_create failed");
+    }
+    HIP_TRY(hipHostMalloc((void **)&o.karg, 512 * kAqlOneSlots, hipHostMallocMapped | hipHostMallocCoherent));
+    o.device = t_ctx.device;
+  }
+  const AqlKernel &k = o.dev->k[id];
+  if (k.kernarg > 512u) return set_err(-EPROTO, "AQL engine: kernarg segment %u B", k.kernarg);
+  // the previous dispatch has completed (synchronous), so any slot is free;
+  // rotating keeps a slot from being rewritten while a late reader might hold it
+  uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
+  memset(ka, 0, k.kernarg);
+  aql_fill_args(ka, args, blocks);
+  hsa_kernel_dispatch_packet_t t;
+  aql_fill_packet(t, k, blocks, ka);
+  hsa_signal_store_relaxed(o.sig, 1);
+  const uint64_t idx = hsa_queue_add_write_index_screlease(o.q, 1);
+  while (idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
+  }
+  hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (idx & (o.q->size - 1));
+  memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
+  slot->completion_signal = o.sig;
+  const uint32_t hs = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
+                      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) | ((uint32_t)t.setup << 16);
+  __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
+  timespec ts0, ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts0);
+  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
+    if (g_aql_queue_error.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", g_aql_queue_error.load());
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    if (ts.tv_sec - ts0.tv_sec > 10) return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
+  }
   return 0;
 }
 
@@ -3887,11 +3969,28 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   // Over PCIe a whole wave per datagram (64 x 4: 1 KiB contiguous per
   // wave-instruction, 4 KiB per pass) reads fastest: 48 GiB/s of 1500 B
   // slots against 43 for the HBM-tuned 16 x 6 (tools/host_sweep.py).
-  int rc = !b->offs && !b->lens && b->fixed_len >= 512 && !g_tune.g
-               ? launch_verify_shape(d, Shape{64, 4}, zip, zl4, zst, zbad, st)
-               : launch_verify(d, max_len, zip, zl4, zst, zbad, st);
-  if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(st));
+  const bool wide = !b->offs && !b->lens && b->fixed_len >= 512 && !g_tune.g;
+  // One dispatch through the AQL engine (MI_CKSUM_HOST_AQL=0: HIP launch +
+  // stream synchronize): a burst costs one packet and one spin, not a HIP
+  // launch and its completion processing (profiles/burst_r02.jsonl).
+  static const bool host_aql = [] {
+    const char *e = getenv("MI_CKSUM_HOST_AQL");
+    return !(e && e[0] == '0');
+  }();
+  int id = -1;
+  unsigned blocks = 0;
+  AqlDevice *adv = nullptr;
+  if (host_aql && aql_device(t_ctx.device, &adv) == 0 &&
+      (wide ? aql_kernel_for_shape(d, Shape{64, 4}, &id, &blocks)
+                        : aql_kernel_for(d, max_len, &id, &blocks)) == 0) {
+    int rc = aql_one_dispatch(id, blocks, AqlArgs{d, zip, zl4, zst, zbad});
+    if (rc) return rc;
+  } else {
+    int rc = wide ? launch_verify_shape(d, Shape{64, 4}, zip, zl4, zst, zbad, st)
+                  : launch_verify(d, max_len, zip, zl4, zst, zbad, st);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+  }
   if (o.ip) memcpy(o.ip, h + o_ip, 2 * n);
   if (o.l4) memcpy(o.l4, h + o_l4, 2 * n);
   if (o.st) memcpy(o.st, h + o_st, n);
