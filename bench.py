@@ -270,7 +270,9 @@ def main():
             traffic = None
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
-                kernel=mi.verify_plan(batches[0]), alg_bytes_per_launch=int(alg_bytes),
+                kernel=mi.verify_plan(batches[0]) + (" (its AQL entry point mi_aql_*)" if rep is not None and
+                                                     getattr(rep, "engine", "hip") == "aql" else ""),
+                alg_bytes_per_launch=int(alg_bytes),
                 avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst,
                 wall_frac=round(alg_bytes * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))
     # the same kernel alone on one stream, every launch bracketed by events
