@@ -1783,6 +1783,15 @@ __device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, cons
 // load that would start before the source buffer or run past its end takes a
 // per-byte path instead (the first / last bytes of the buffer only).
 constexpr int kTxSeg = 4;
+// MI_TX_PIPE=1: the frame's passes software-pipelined (below).  Measured on
+// MI355X (profiles/tx_pipe_r02.jsonl, same box, interleaved): socket frames
+// 57.9 us per launch against 51.3 one pass at a time, single-segment frames
+// 55.2 vs 48.3 -- the second pass of loads pushes the 128-VGPR bound into
+// 52 B/lane of scratch spills and the per-chunk cut is computed twice -- so
+// it is off.
+#ifndef MI_TX_PIPE
+#define MI_TX_PIPE 0
+#endif
 
 // A frame's first kTxSeg nonempty segments: segment e covers frame bytes
 // [S_e, S_e+1) (S_0 = 0, the last one to L), frame byte q of segment e sits
@@ -2090,6 +2099,38 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
       const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
       u32x4 held{0, 0, 0, 0};
+#if MI_TX_PIPE
+      // Software pipeline over the frame's passes: pass p+1's loads are issued
+      // before pass p is built, folded and stored, so a group keeps a pass of
+      // loads in flight while it computes (the kernel waited on memory 53 % of
+      // its wave cycles with one pass at a time, profiles/pmc_tx_shapes_r02.jsonl).
+      // The cut of a chunk is recomputed at build time instead of being held
+      // (registers: U <= 2 shapes are bounded to 128).  Past the last pass
+      // the loads get the out-of-range offset (no traffic).
+      u32x4 xa[U], xb[U];
+      auto issue = [&](uint32_t p, u32x4 (&a)[U], u32x4 (&b)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
+          const bool in = p < npass && !c.slow;
+          a[u] = ld16(rs, in && c.q0 < sg.L ? c.A1 : kOOB);
+          b[u] = ld16(rs, in && c.two ? c.A2 : kOOB);
+        }
+      };
+      issue(0, xa, xb);
+      for (uint32_t p = 0; p < npass; ++p) {
+        u32x4 v[U];
+        u32x4 ya[U], yb[U];
+        issue(p + 1, ya, yb);
+        if (p == 0) prefetch2();
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          xa[u] = ya[u];
+          xb[u] = yb[u];
+        }
+#else
       for (uint32_t p = 0; p < npass; ++p) {
         u32x4 v[U];
         u32x4 xa[U], xb[U];
@@ -2104,6 +2145,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         if (p == 0) prefetch2();
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
+#endif
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;

@@ -4,13 +4,13 @@
 # as the reference point.  Interleaved rounds.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/aql
+O=gpurun_out/aql${SWEEP_TAG:-}
 mkdir -p $O
 mv -f $O/sweep.jsonl $O/sweep_prev.jsonl 2>/dev/null
 # (first pass, barrier bit 0: one queue 17.9 us per pass, two 15.0-15.2, HIP
 # 14.7-15.0; agent vs system release no difference)
 VARIANTS=(${AQL_VARIANTS:-"launch:2:system:1" "aql:2:system:1" "aql:2:system:0" "aql:3:system:1" "aql:4:system:1"})
-for round in 1 2 3; do
+for round in $(seq 1 ${ROUNDS:-3}); do
   for v in "${VARIANTS[@]}"; do
     IFS=: read sub ns rel bar <<< "$v"
     echo "== $round $v"
