@@ -1126,6 +1126,13 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uin
 // hands lane k its own slot's four chunks, and the lane folds its datagram
 // directly -- no scan, no per-datagram header / tail reloads (which cost the
 // flat-run kernel four scattered 16-byte L2 requests per datagram).
+// MI_SLOT64_PREFETCH=1: each wave's next 64-slot range is loaded while the
+// current one is folded.  Measured (profiles/slot64_pf_r02.jsonl, same box,
+// interleaved, 2^20 slots): 11.64-11.73 us per batch at the default grid cap
+// against 11.36-11.48 without -- off.
+#ifndef MI_SLOT64_PREFETCH
+#define MI_SLOT64_PREFETCH 0
+#endif
 __device__ __forceinline__ void slot64_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad) {
   __shared__ u32x4 s_slot[kBlock / 64][256];
@@ -1136,14 +1143,27 @@ __device__ __forceinline__ void slot64_body(const Desc &d, uint16_t *ip_out, uin
   const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
   u32x4 *sl = s_slot[wv];
   VOut pend;  // the previous range's outputs, emitted behind this range's loads
-  for (uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u; p0 < d.n; p0 += rstride) {
-    const uint32_t base = slot0 + 64u * p0, nslot = min(64u, d.n - p0);
-    u32x4 v[4];
+  // the 4 KiB of a 64-slot range: four fully coalesced 1 KiB wave-loads
+  auto issue = [&](uint32_t q0, u32x4 (&v)[4]) {
+    const uint32_t base = slot0 + 64u * q0, nslot = q0 < d.n ? min(64u, d.n - q0) : 0u;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t c = 64u * u + lane;  // chunk of the range: slot c / 4
       v[u] = ld16(r, c < 4u * nslot ? base + 16u * c : kOOB);
     }
+  };
+  uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u;
+  if (p0 >= d.n) return;
+  u32x4 v[4];
+  issue(p0, v);
+  for (;;) {
+    const uint32_t base = slot0 + 64u * p0, pn = p0 + rstride;
+#if MI_SLOT64_PREFETCH
+    // the wave's next range is loaded while this one is folded (waves loop
+    // over several ranges: the grid is capped, slot64_blocks)
+    u32x4 vn[4];
+    issue(pn, vn);
+#endif
     verify_emit(pend, ip_out, l4_out, st_out, bad, d);
     pend.i = ~0u;
 #pragma unroll
@@ -1176,6 +1196,14 @@ __device__ __forceinline__ void slot64_body(const Desc &d, uint16_t *ip_out, uin
         pend.i = ~0u;
       }
     }
+    if (pn >= d.n) break;
+    p0 = pn;
+#if MI_SLOT64_PREFETCH
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = vn[u];
+#else
+    issue(p0, v);
+#endif
   }
   verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
@@ -2583,8 +2611,12 @@ unsigned run_blocks(const Desc &d) {
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
 }
+// 64 B slots: at most 1024 blocks (4096 waves, each looping over its
+// ranges) -- profiles/slot64_cap_r02.jsonl, slot64_pf_r02.jsonl: one range
+// per wave (cap 16384) 13.4-13.75 us per 2^20-slot batch, cap 1024 11.4-11.6,
+// 2048 11.4-11.8, 512 12.5-12.8.
 unsigned slot64_blocks(const Desc &d) {
-  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 1024;
   uint64_t blocks = ((uint64_t)d.n + 255) / 256;
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
