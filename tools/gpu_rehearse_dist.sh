@@ -6,9 +6,12 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for cfg in 1500 pareto; do
+for np in ${NPROCS:-2}; do
+for cfg in ${CONFIGS:-1500 pareto}; do
   MI_BENCH_DEVICE=0 MI_BENCH_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 \
-    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config $cfg \
-    --steps 200 --warmup 20 > gpurun_out/dist2_$cfg.json 2> gpurun_out/dist2_$cfg.err || exit $?
+    --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus $np --config $cfg \
+    --steps ${STEPS:-200} --warmup 20 > gpurun_out/dist${np}_$cfg.json 2> gpurun_out/dist${np}_$cfg.err || exit $?
+  cut -c1-400 gpurun_out/dist${np}_$cfg.json
+done
 done
 echo "exit 0"
