@@ -2225,7 +2225,34 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
 // caller's pinned slot with a system-scope store, tagged so the host can spin
 // on it (mi__scalar_fold) instead of waiting for the stream.
 constexpr int kScalarThreads = 512;
-__global__ __launch_bounds__(kScalarThreads) void k_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
+
+}  // namespace
+
+// AQL entry points (the repeat handle's AQL engine, MI_REPEAT_ENGINE_AQL): the
+// RX verify kernels again, under extern "C" names, so the engine can find their
+// kernel descriptors by name in the code object HIP loaded and dispatch them
+// with packets it writes itself.  One argument list for all of them.
+#define MI_AQL_SHAPE(G_, U_)                                                                            \
+  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_v_##G_##x##U_(                           \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
+    verify_body<G_, U_>(d, ip, l4, st, bad);                                                            \
+  }
+#define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12) X(64, 4)
+MI_AQL_SHAPES(MI_AQL_SHAPE)
+#define MI_AQL_RUN(U_)                                                                                  \
+  extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
+                                                           uint32_t *bad) {                             \
+    packed_body<U_, 0>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                                            \
+  }
+MI_AQL_RUN(4)
+MI_AQL_RUN(8)
+MI_AQL_RUN(16)
+extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st,
+                                                                   uint32_t *bad) {
+  slot64_body(d, ip, l4, st, bad);
+}
+// (the same kernel serves the HIP launch and the AQL one-shot dispatch, hence extern "C")
+extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
                                                           uint32_t len, uint32_t abs_lanes, int pseudo,
                                                           uint32_t src, uint32_t dst, uint32_t proto,
                                                           uint32_t plen, uint32_t tag, uint32_t *out) {
@@ -2265,31 +2292,6 @@ __global__ __launch_bounds__(kScalarThreads) void k_scalar(const uint8_t *base, 
   }
 }
 
-}  // namespace
-
-// AQL entry points (the repeat handle's AQL engine, MI_REPEAT_ENGINE_AQL): the
-// RX verify kernels again, under extern "C" names, so the engine can find their
-// kernel descriptors by name in the code object HIP loaded and dispatch them
-// with packets it writes itself.  One argument list for all of them.
-#define MI_AQL_SHAPE(G_, U_)                                                                            \
-  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_v_##G_##x##U_(                           \
-      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
-    verify_body<G_, U_>(d, ip, l4, st, bad);                                                            \
-  }
-#define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12) X(64, 4)
-MI_AQL_SHAPES(MI_AQL_SHAPE)
-#define MI_AQL_RUN(U_)                                                                                  \
-  extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
-                                                           uint32_t *bad) {                             \
-    packed_body<U_, 0>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                                            \
-  }
-MI_AQL_RUN(4)
-MI_AQL_RUN(8)
-MI_AQL_RUN(16)
-extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st,
-                                                                   uint32_t *bad) {
-  slot64_body(d, ip, l4, st, bad);
-}
 
 namespace {
 
@@ -2773,18 +2775,19 @@ enum AqlKernelId {
 #define X(G_, U_) kAqlV_##G_##x##U_,
   MI_AQL_SHAPES(X)
 #undef X
-  kAqlRun4, kAqlRun8, kAqlRun16, kAqlSlot64, kAqlKernels
+  kAqlRun4, kAqlRun8, kAqlRun16, kAqlSlot64, kAqlScalar, kAqlKernels
 };
 const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
     MI_AQL_SHAPES(X)
 #undef X
-    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_slot64"};
+    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_slot64", "mi_aql_scalar"};
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
 #undef X
-    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_slot64};
+    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_slot64,
+    (const void *)mi_aql_scalar};
 
 // The kernels' explicit arguments, laid out as the compiler lays out the
 // kernel-argument segment (each parameter at its natural alignment).  The
@@ -2914,9 +2917,9 @@ int aql_device(int dev, AqlDevice **out) {
         (void)ldr.hsa_ven_amd_loader_iterate_executables(aql_exe_cb, &f);
       for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
         if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
-        else if (a.k[i].kernarg < kAqlHidden || a.k[i].kernarg > 1024u)
+        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : kAqlHidden + 66u) || a.k[i].kernarg > 512u)
           fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
-               (unsigned)sizeof(AqlArgs));
+               i == kAqlScalar ? 56u : (unsigned)sizeof(AqlArgs));
       }
     }
   }
@@ -3009,24 +3012,32 @@ void aql_free(AqlRun *a) {
 // grid dimensions (AMDGPUUsage "hidden_*"; offsets checked against the
 // kernels' metadata: hidden_block_count_x at 112 = kAqlHidden, _group_size_x
 // +12, _remainder_x +18, _grid_dims +64).  The rest of the block is zero.
-void aql_fill_args(uint8_t *ka, const AqlArgs &args, unsigned blocks) {
-  memcpy(ka, &args, sizeof args);
-  uint8_t *h = ka + kAqlHidden;
+// (a kernel that reads no hidden argument -- mi_aql_scalar -- has a segment of
+// just its explicit arguments: then nothing is written past them)
+void aql_fill_raw(uint8_t *ka, const void *args, uint32_t nargs, unsigned blocks, unsigned wg, uint32_t segment) {
+  memcpy(ka, args, nargs);
+  if (segment < ((nargs + 7u) & ~7u) + 66u) return;
+  uint8_t *h = ka + ((nargs + 7u) & ~7u);
   const uint32_t bc[3] = {blocks, 1u, 1u};
-  const uint16_t gs[3] = {(uint16_t)kBlock, 1u, 1u}, rem[3] = {0, 0, 0}, dims = 1;
+  const uint16_t gs[3] = {(uint16_t)wg, 1u, 1u}, rem[3] = {0, 0, 0}, dims = 1;
   memcpy(h + 0, bc, sizeof bc);
   memcpy(h + 12, gs, sizeof gs);
   memcpy(h + 18, rem, sizeof rem);
   memcpy(h + 64, &dims, sizeof dims);
 }
+void aql_fill_args(uint8_t *ka, const AqlArgs &args, unsigned blocks) {
+  static_assert(kAqlHidden == ((sizeof(AqlArgs) + 7u) & ~7u), "hidden arguments follow the explicit ones");
+  aql_fill_raw(ka, &args, sizeof args, blocks, kBlock, ~0u);
+}
 // A dispatch packet without its header (written last, at submission).
-void aql_fill_packet(hsa_kernel_dispatch_packet_t &p, const AqlKernel &k, unsigned blocks, void *kargs) {
+void aql_fill_packet(hsa_kernel_dispatch_packet_t &p, const AqlKernel &k, unsigned blocks, void *kargs,
+                     unsigned wg = kBlock) {
   memset(&p, 0, sizeof p);
   p.setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;
-  p.workgroup_size_x = (uint16_t)kBlock;
+  p.workgroup_size_x = (uint16_t)wg;
   p.workgroup_size_y = 1;
   p.workgroup_size_z = 1;
-  p.grid_size_x = blocks * (uint32_t)kBlock;
+  p.grid_size_x = blocks * wg;
   p.grid_size_y = 1;
   p.grid_size_z = 1;
   p.private_segment_size = k.priv;
@@ -3198,7 +3209,10 @@ void aql_one_release(AqlOne &o) {
   o = AqlOne();
 }
 
-int aql_one_dispatch(int id, unsigned blocks, const AqlArgs &args) {
+// nargs explicit argument bytes at args (laid out like the kernel's
+// parameters); wait: spin on the completion signal (else the kernel signals
+// the caller itself, e.g. through a pinned host word)
+int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait) {
   AqlOne &o = t_aql1;
   if (o.device != t_ctx.device) {
     aql_one_release(o);
@@ -3222,21 +3236,22 @@ int aql_one_dispatch(int id, unsigned blocks, const AqlArgs &args) {
   // rotating keeps a slot from being rewritten while a late reader might hold it
   uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
   memset(ka, 0, k.kernarg);
-  aql_fill_args(ka, args, blocks);
+  aql_fill_raw(ka, args, nargs, blocks, wg, k.kernarg);
   hsa_kernel_dispatch_packet_t t;
-  aql_fill_packet(t, k, blocks, ka);
-  hsa_signal_store_relaxed(o.sig, 1);
+  aql_fill_packet(t, k, blocks, ka, wg);
+  if (wait) hsa_signal_store_relaxed(o.sig, 1);
   const uint64_t idx = hsa_queue_add_write_index_screlease(o.q, 1);
   while (idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
   }
   hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (idx & (o.q->size - 1));
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
-  slot->completion_signal = o.sig;
+  slot->completion_signal = wait ? o.sig : hsa_signal_t{0};
   const uint32_t hs = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
                       (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
                       (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) | ((uint32_t)t.setup << 16);
   __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
+  if (!wait) return 0;
   timespec ts0, ts;
   clock_gettime(CLOCK_MONOTONIC, &ts0);
   while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
@@ -4057,7 +4072,8 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   if (host_aql && aql_device(t_ctx.device, &adv) == 0 &&
       (wide ? aql_kernel_for_shape(d, Shape{64, 4}, &id, &blocks)
                         : aql_kernel_for(d, max_len, &id, &blocks)) == 0) {
-    int rc = aql_one_dispatch(id, blocks, AqlArgs{d, zip, zl4, zst, zbad});
+    const AqlArgs args{d, zip, zl4, zst, zbad};
+    int rc = aql_one_submit(id, blocks, kBlock, &args, sizeof args, true);
     if (rc) return rc;
   } else {
     int rc = wide ? launch_verify_shape(d, Shape{64, 4}, zip, zl4, zst, zbad, st)
@@ -4302,10 +4318,32 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   }
   c.stag = (c.stag + 1) & 0xffffu;
   const uint32_t tag = c.stag;
-  hipLaunchKernelGGL(k_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
-                     (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,
-                     (uint32_t)proto, plen, tag, c.sout_dev);
-  HIP_TRY(hipGetLastError());
+  // One dispatch packet into the thread's HSA queue (MI_CKSUM_HOST_AQL=0: a
+  // HIP launch); either way the kernel stores the tagged result straight into
+  // the pinned word spun on below.
+  struct ScalarArgs {  // mi_aql_scalar's parameters, in order
+    const uint8_t *base;
+    uint32_t bytes, off, len, abs_lanes;
+    int pseudo;
+    uint32_t src, dst, proto, plen, tag;
+    uint32_t *out;
+  };
+  static_assert(sizeof(ScalarArgs) == 56, "kernel-argument layout of mi_aql_scalar");
+  static const bool host_aql = [] {
+    const char *e = getenv("MI_CKSUM_HOST_AQL");
+    return !(e && e[0] == '0');
+  }();
+  AqlDevice *adv = nullptr;
+  if (host_aql && aql_device(c.device, &adv) == 0) {
+    const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
+                        lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst, (uint32_t)proto, plen, tag, c.sout_dev};
+    if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false))) return rc;
+  } else {
+    hipLaunchKernelGGL(mi_aql_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
+                       (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,
+                       (uint32_t)proto, plen, tag, c.sout_dev);
+    HIP_TRY(hipGetLastError());
+  }
   volatile uint32_t *slot = c.sout;
   uint32_t v = 0;
   for (uint64_t spin = 0;; ++spin) {
