@@ -3212,7 +3212,10 @@ void aql_one_release(AqlOne &o) {
 // nargs explicit argument bytes at args (laid out like the kernel's
 // parameters); wait: spin on the completion signal (else the kernel signals
 // the caller itself, e.g. through a pinned host word)
-int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait) {
+// sys: acquire / release at system scope (host-memory data the kernel reads
+// through caches or writes with plain stores); else agent scope
+int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait,
+                   bool sys = true) {
   AqlOne &o = t_aql1;
   if (o.device != t_ctx.device) {
     aql_one_release(o);
@@ -3246,9 +3249,10 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (idx & (o.q->size - 1));
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
   slot->completion_signal = wait ? o.sig : hsa_signal_t{0};
+  const uint32_t sc = sys ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
   const uint32_t hs = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
-                      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                      (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) | ((uint32_t)t.setup << 16);
+                      (sc << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (sc << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) |
+                      ((uint32_t)t.setup << 16);
   __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
   if (!wait) return 0;
@@ -4337,7 +4341,15 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   if (host_aql && aql_device(c.device, &adv) == 0) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
                         lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst, (uint32_t)proto, plen, tag, c.sout_dev};
-    if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false))) return rc;
+    // agent-scope fences (MI_CKSUM_SCALAR_SYS=1: system): the kernel reads the
+    // staging bytes from fine-grained (uncached) pinned memory and hands its
+    // result over with its own system-scope atomic store, so the packet needs
+    // no system-wide cache maintenance around it
+    static const bool sys = [] {
+      const char *e = getenv("MI_CKSUM_SCALAR_SYS");
+      return e && e[0] == '1';
+    }();
+    if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false, sys))) return rc;
   } else {
     hipLaunchKernelGGL(mi_aql_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
                        (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,

@@ -14,12 +14,13 @@ tail -2 $O/tests.log
 fi
 rm -f $O/lat.jsonl
 for round in 1 2; do
-  for aql in 1 0; do
-    MI_CKSUM_HOST_AQL=$aql timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-host-path > $O/b.json 2>> $O/b.err || exit 1
+  for aql in ${DROPIN_VARIANTS:-1 0}; do
+    e="MI_CKSUM_HOST_AQL=1"; [ "$aql" = 0 ] && e="MI_CKSUM_HOST_AQL=0"; [ "$aql" = sys ] && e="MI_CKSUM_SCALAR_SYS=1"
+    env $e timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --cpu-seconds 0 --no-host-path > $O/b.json 2>> $O/b.err || exit 1
     python - "$aql" $O/b.json >> $O/lat.jsonl <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read())
-print(json.dumps(dict(host_aql=int(sys.argv[1]), value=d["value"], dropin=d.get("dropin_latency"))))
+print(json.dumps(dict(host_aql=sys.argv[1], value=d["value"], dropin=d.get("dropin_latency"))))
 PY
     tail -1 $O/lat.jsonl | cut -c1-400
   done
