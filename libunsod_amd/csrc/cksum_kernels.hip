@@ -4341,13 +4341,15 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   if (host_aql && aql_device(c.device, &adv) == 0) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
                         lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst, (uint32_t)proto, plen, tag, c.sout_dev};
-    // agent-scope fences (MI_CKSUM_SCALAR_SYS=1: system): the kernel reads the
-    // staging bytes from fine-grained (uncached) pinned memory and hands its
-    // result over with its own system-scope atomic store, so the packet needs
-    // no system-wide cache maintenance around it
+    // system-scope fences: the staging buffer is ordinary (non-coherent)
+    // pinned memory rewritten by the host every call, so the GPU's caches must
+    // not keep its old lines.  MI_CKSUM_SCALAR_SYS=0 tries agent scope
+    // (measured 0.8 us faster per call, profiles/dropin_aql_r02.jsonl) -- not
+    // the default: it is only safe for fine-grained staging, and the round-2
+    // closing suite hit a GPU memory fault with it on (cause not isolated).
     static const bool sys = [] {
       const char *e = getenv("MI_CKSUM_SCALAR_SYS");
-      return e && e[0] == '1';
+      return !(e && e[0] == '0');
     }();
     if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false, sys))) return rc;
   } else {
