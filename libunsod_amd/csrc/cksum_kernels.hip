@@ -3405,11 +3405,27 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
   a.nb = nb;
   a.units = units;
   if (!units) return 0;
-  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 2048;
+  // Grid: as many blocks as can be resident at once (occupancy x CUs), so
+  // every wave streams its units from the start to the end of the launch.  A
+  // larger grid (round 1: 2048 blocks of which ~1280 fit) runs in two rounds:
+  // the late blocks start only when early ones have finished ALL their units,
+  // and the second round runs at partial occupancy (18-19 us per 1500 B batch
+  // against 14.2 for overlapped single launches, profiles/multi_r02.jsonl).
+  // MI_CKSUM_MAX_BLOCKS caps it instead (the old behaviour).
   uint64_t blocks = ((uint64_t)units + (kBlock / 64) - 1) / (kBlock / 64);
-  if (blocks > (uint64_t)cap) blocks = cap;
+  auto resident = [&](const void *fn) -> uint64_t {
+    int per_cu = 0, dev = t_ctx.device;
+    hipDeviceProp_t prop;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) != hipSuccess || per_cu <= 0 ||
+        hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return 2048;
+    return (uint64_t)per_cu * (uint64_t)prop.multiProcessorCount;
+  };
 #define X(G_, U_)                                                                                 \
   if (sh.g == G_ && sh.u == U_) {                                                                 \
+    static const uint64_t res_ = resident((const void *)k_ipv4_verify_multi<G_, U_>);           \
+    const uint64_t cap_ = g_tune.max_blocks > 0 ? (uint64_t)g_tune.max_blocks : res_;             \
+    if (blocks > cap_) blocks = cap_;                                                             \
     VLAUNCH((k_ipv4_verify_multi<G_, U_>), dim3((unsigned)blocks), dim3(kBlock), 0, s, a);       \
     return launched();                                                                            \
   }

@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--config", default="1500")
     ap.add_argument("--ms", default="1,2,4,8,16")
     ap.add_argument("--batches", type=int, default=320, help="batches verified per measurement")
-    ap.add_argument("--caps", default="0", help="workgroup caps to sweep (0: the library default, 2048)")
+    ap.add_argument("--caps", default="0", help="workgroup caps to sweep (0: the library default -- a resident-sized grid for "
+                                                "the multi-batch launch, 2048 for single launches)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L, stride, first = CFG[a.config]
@@ -70,7 +71,7 @@ def main():
             e1.record(s)
         s.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / (launches * m)
-        print(json.dumps(dict(config=a.config, batches_per_launch=m, launches=launches, streams=1, cap=cap or 2048,
+        print(json.dumps(dict(config=a.config, batches_per_launch=m, launches=launches, streams=1, cap=cap or "default",
                               us_per_batch=round(us, 3), frac=round(alg / us / 8e6, 4),
                               GiBps=round(n * L / (us * 1e-6) / 2**30, 1))), flush=True)
 
