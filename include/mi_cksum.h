@@ -21,7 +21,8 @@
  * Results are bit-identical to the reference on the same bytes at the same
  * addresses (address parity matters only for in_cksum_hdr, in_cksum.c:278-285).
  * There is no CPU fallback: without a usable gfx950 device the batch calls
- * return -ENODEV and the (b1) calls abort with a message.
+ * return -ENODEV and the (b1) calls abort with a message (or, with
+ * mi_cksum_set_dropin_error_handler, report and return 0xffff).
  */
 #ifndef MI_CKSUM_H
 #define MI_CKSUM_H
@@ -62,6 +63,19 @@ unsigned short in_pseudo(unsigned int a, unsigned int b, unsigned int c);
 /* in_cksum.c:172-179 -- one's-complement add of two u16. */
 unsigned short in_addword(unsigned short a, unsigned short b);
 
+/* (b1) error policy.  The reference's functions cannot fail and return only
+ * the sum, so a drop-in whose GPU dispatch fails (no device, a queue error, no
+ * result within 10 s) prints the error and aborts by default: any value it
+ * returned would be a wrong checksum.  A handler installed here is called
+ * instead with the function name and mi_cksum_strerror(), and the call
+ * returns 0xffff.  No datagram with valid sums verifies to 0xffff (valid ones
+ * verify to 0; ~fold(S) is 0xffff only for all-zero bytes), so an RX caller
+ * (ip_input.c:463-469, tcp_input.c:716-720) drops the packet.  On TX the
+ * value is stored into the outgoing header like any other result.  NULL
+ * restores the default.  Process-wide. */
+typedef void (*mi_cksum_error_fn)(const char *what, const char *err);
+void mi_cksum_set_dropin_error_handler(mi_cksum_error_fn fn);
+
 /* ------------------------------------------------------------------------ */
 /* runtime                                                                    */
 /* ------------------------------------------------------------------------ */
@@ -74,6 +88,10 @@ int mi_cksum_init(int device);
 /* Text of the last error on this thread ("" if none). */
 const char *mi_cksum_strerror(void);
 const char *mi_cksum_version(void);
+/* Diagnostics: HSA queues the library holds right now -- two (nstreams) per
+ * AQL-engine repeat handle, one per thread that made a drop-in or host-burst
+ * call (given back when that thread exits or moves to another device). */
+int mi_cksum_hsa_queues(void);
 
 /* Tuning knob (process-wide): force the lane-group shape -- `group` lanes per
  * packet, `chunks` 16-byte loads per lane per pass -- and cap the grid at

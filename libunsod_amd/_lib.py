@@ -161,7 +161,12 @@ SIGNATURES = {
     "mi_cksum_host_register": (C.c_int, [C.c_void_p, C.c_uint64]),
     "mi_cksum_host_unregister": (C.c_int, [C.c_void_p]),
     "mi_cksum_synth_ipv4": (C.c_int, [C.POINTER(PktBatchC), C.c_uint64, C.c_void_p]),
+    "mi_cksum_hsa_queues": (C.c_int, []),
+    "mi_cksum_set_dropin_error_handler": (None, [C.c_void_p]),
 }
+
+# mi_cksum_error_fn: void (*)(const char *what, const char *err)
+DROPIN_ERROR_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_char_p)
 
 _lib = None
 

@@ -13,9 +13,13 @@
  * are absolute (in_cksum.c:278-285).
  *
  * in_pseudo / in_addword fold two or three integers and touch no packet bytes;
- * they are computed here.  There is no CPU path for byte folding: if the GPU is
- * unusable the call aborts with a message (the reference API has no error
- * return).
+ * they are computed here.  There is no CPU path for byte folding.  If the GPU
+ * is unusable the call has no way to say so (the reference API has no error
+ * return), so by default it aborts with a message: every value it could return
+ * instead is a wrong checksum.  An embedder may install
+ * mi_cksum_set_dropin_error_handler: the handler is told, and the call returns
+ * 0xffff -- never the result of verifying a datagram with valid sums (those
+ * verify to 0), so an RX caller drops the packet.
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -35,6 +39,24 @@ _Static_assert(offsetof(struct mi_mbuf_view, m_data) == 16, "m_data@16 (mbuf.h:9
 _Static_assert(offsetof(struct mi_mbuf_view, m_len) == 24, "m_len@24 (mbuf.h:94)");
 
 /* Visit the (addr, len) spans in_cksum_skip would fold, in stream order. */
+static mi_cksum_error_fn g_dropin_handler;
+
+void mi_cksum_set_dropin_error_handler(mi_cksum_error_fn fn)
+{
+	__atomic_store_n(&g_dropin_handler, fn, __ATOMIC_RELEASE);
+}
+
+/* The (b1) error policy: abort, or the installed handler and 0xffff. */
+static uint16_t dropin_fail(const char *what)
+{
+	mi_cksum_error_fn fn = __atomic_load_n(&g_dropin_handler, __ATOMIC_ACQUIRE);
+
+	if (!fn)
+		mi__fatal(what);
+	fn(what, mi_cksum_strerror());
+	return 0xffff;
+}
+
 static long walk_skip(const struct mi_mbuf_view *m, long len, long skip, uint8_t *dst)
 {
 	long total = 0, rem = len - skip;
@@ -105,10 +127,10 @@ unsigned short in_cksum_skip(struct mbuf *m0, int len, int skip)
 	uint16_t r;
 
 	if (!st)
-		mi__fatal("in_cksum_skip");
+		return dropin_fail("in_cksum_skip");
 	walk_skip(m, len, skip, st);
 	if (mi__scalar_fold(0, (uint32_t)total, MI_SPAN_STREAM, 0, 0, 0, 0, 0, &r))
-		mi__fatal("in_cksum_skip");
+		return dropin_fail("in_cksum_skip");
 	return r;
 }
 
@@ -121,11 +143,11 @@ uint16_t in_cksum_pseudo_header(struct mbuf *m0, int plen, int off0, uint32_t sr
 	uint16_t r;
 
 	if (!st)
-		mi__fatal("in_cksum_pseudo_header");
+		return dropin_fail("in_cksum_pseudo_header");
 	walk_pseudo(m, plen, off0, st);
 	if (mi__scalar_fold(0, (uint32_t)total, MI_SPAN_STREAM, 1, src, dst, protonum,
 	                    (uint32_t)plen, &r))
-		mi__fatal("in_cksum_pseudo_header");
+		return dropin_fail("in_cksum_pseudo_header");
 	return r;
 }
 
@@ -136,10 +158,10 @@ unsigned int in_cksum_hdr(const struct ip *ip)
 	uint16_t r;
 
 	if (!st)
-		mi__fatal("in_cksum_hdr");
+		return dropin_fail("in_cksum_hdr");
 	memcpy(st + mod, ip, 20);
 	if (mi__scalar_fold(mod, 20, MI_SPAN_ABS, 0, 0, 0, 0, 0, &r))
-		mi__fatal("in_cksum_hdr");
+		return dropin_fail("in_cksum_hdr");
 	return r;
 }
 

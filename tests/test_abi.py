@@ -93,3 +93,25 @@ def test_verify_plan_needs_no_gpu():
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8>"
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens)) == "k_ipv4_verify x length classes"
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens // 4)) == "k_ipv4_verify<1,8>"
+
+
+@pytest.mark.skipif(mi.device_count() > 0, reason="a GPU is present")
+def test_dropin_error_handler_returns_bad_sum():
+    """With a handler installed, a drop-in that cannot reach the GPU reports
+    through it and returns 0xffff (what no datagram with valid sums verifies
+    to), instead of aborting; resetting the handler restores the abort."""
+    from libunsod_amd._lib import DROPIN_ERROR_FN
+    seen = []
+    cb = DROPIN_ERROR_FN(lambda what, err: seen.append((what.decode(), err.decode())))
+    lib = load()
+    lib.mi_cksum_set_dropin_error_handler(C.cast(cb, C.c_void_p))
+    try:
+        m = mi.MbufChain([bytes(range(64))])
+        assert mi.in_cksum_skip(m, 64, 0) == 0xFFFF
+        assert mi.in_cksum_hdr(bytes(20)) == 0xFFFF
+        assert mi.in_cksum_pseudo_header(m, 44, 20, 1, 2, 6) == 0xFFFF
+        assert [w for w, _ in seen] == ["in_cksum_skip", "in_cksum_hdr", "in_cksum_pseudo_header"]
+        assert all(e for _, e in seen)
+    finally:
+        lib.mi_cksum_set_dropin_error_handler(None)
+    assert lib.mi_cksum_hsa_queues() == 0

@@ -69,3 +69,36 @@ def test_aql_entry_points_kernarg_layout(tmp_path):
         for o, s, k in args:
             if k in HIDDEN:
                 assert o == SCALAR_EXPLICIT + HIDDEN[k], ("mi_aql_scalar", k, o)
+
+
+def _all_kernel_notes(tmp_path):
+    if not (os.path.exists(BUNDLER) and os.path.exists(READELF) and shutil.which("objcopy")):
+        pytest.skip("LLVM / binutils tools not available")
+    fat = tmp_path / "fatbin_all.bin"
+    co = tmp_path / "co_all.elf"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB_PATH, str(fat)], check=True)
+    subprocess.run([BUNDLER, "--unbundle", "--type=o", f"--input={fat}",
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+    notes = subprocess.run([READELF, "--notes", str(co)], check=True, capture_output=True, text=True).stdout
+    out = {}
+    for block in re.split(r"\n  - \.agpr_count:", notes)[1:]:
+        name = re.search(r"\.name:\s+(\S+)", block).group(1)
+        priv = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", block).group(1))
+        dyn = re.search(r"\.uses_dynamic_stack:\s+(\w+)", block).group(1)
+        out[name] = (priv, dyn)
+    return out
+
+
+def test_no_kernel_uses_scratch(tmp_path):
+    """Every kernel of the library runs without a private segment (scratch).
+    Round 2's k_ipv4_finalize<BLOCKS> kept its deferred-store state in a
+    12-byte stack object (a pointer select the optimiser made from stores in
+    two branches) and was the only kernel with scratch -- and the one that hit
+    hipErrorIllegalAddress in the driver's suite.  A kernel that picks up
+    scratch again (a dynamically indexed array, an address-taken local) fails
+    here, on the CPU, before it reaches a GPU."""
+    ks = _all_kernel_notes(tmp_path)
+    assert len(ks) > 100, len(ks)
+    assert any("k_ipv4_finalize" in k for k in ks)
+    bad = {k: v for k, v in ks.items() if v != (0, "false")}
+    assert not bad, bad
