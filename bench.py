@@ -69,40 +69,30 @@ def parse():
                          "as K prebuilt AQL packets in the handle's own HSA queue (MI_REPEAT_ENGINE_AQL)")
     ap.add_argument("--settle", type=float, default=0.3,
                     help="untimed warm-up lasts at least this many seconds (GPU clock settle)")
-    return ap.parse_args()
+    ap.add_argument("--also", default="auto",
+                    help="a second config timed in the same run and reported as config_<name> (auto: 9000 when "
+                         "the config is 1500 -- the metric names both frame sizes; none: off)")
+    ap.add_argument("--sustain-seconds", type=float, default=3.0,
+                    help="after the timed region, re-run the same passes back to back this long (reported as "
+                         "'sustained', not part of value; 0 = off)")
+    a = ap.parse_args()
+    if a.also == "auto":
+        a.also = "9000" if a.config == "1500" else ""
+    elif a.also == "none":
+        a.also = ""
+    elif a.also not in list(CONFIGS) + ["pareto"]:
+        ap.error(f"--also {a.also}: unknown config")
+    return a
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # MI_BENCH_DEVICE / MI_BENCH_BACKEND exist only to rehearse the N>1 path on
-    # a one-GPU box (all ranks on one device, gloo); the driver's runs use
-    # LOCAL_RANK and RCCL ("nccl").
-    gpu = int(os.environ.get("MI_BENCH_DEVICE", local))
-    backend = os.environ.get("MI_BENCH_BACKEND", "nccl")
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-
-    import libunsod_amd as mi
-    from libunsod_amd import shard, synth
-    if args.wait == "busy":
-        mi.set_busy_wait(True)
-
-    # ---------------------------------------------------------- workload
-    if args.config == "pareto":
+def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev, rank: int, world: int):
+    """The batches of one config on this rank: R rotating device batches,
+    device-generated and TX-finalized so every packet verifies."""
+    if config == "pareto":
         total_n = 1 << 22
         lens_all = synth.pareto_lengths(total_n)
         lo, hi = shard.shard_by_bytes(lens_all, world, rank)
@@ -114,9 +104,10 @@ def main():
         workload = f"Pareto 64-9000 B IPv4/TCP RX verify, {total_n} packets split by bytes over {world} GPU(s)"
         scaling = "strong"
         cfg = dict(workload=workload, packets_total=total_n, packets_this_rank=n, seed="0x9A7E70", alpha=1.16,
-                   offsets="u64" if args.offs64 else "u32")
+                   offsets="u64" if offs64 else "u32")
+        stride = first = L = None
     else:
-        n, L, stride, first = CONFIGS[args.config]
+        n, L, stride, first = CONFIGS[config]
         lens = offs = None
         L_sum = n * L
         size = first + (n - 1) * stride + L + 64
@@ -129,11 +120,10 @@ def main():
     # a batch (profiles/ceiling_r02.jsonl: at 0.7 GB between reuses 1500 B
     # verify read ~1.5 % faster than at 2.3 GB).
     read_per_batch = min(size, L_sum + 16 * n)
-    R = args.rotate or 1 + -(-(2 << 30) // read_per_batch)
-    cfg.update(streams=args.streams, rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
+    R = rotate or 1 + -(-(2 << 30) // read_per_batch)
+    cfg.update(rotating_batches=R, footprint_MiB=round(R * size / 2**20, 1),
                read_between_reuse_MB=round((R - 1) * read_per_batch / 1e6),
                parallelism=f"dp{world} (independent packet shards, no collective)")
-
     batches, outs = [], []
     for r in range(R):
         buf = torch.empty(size, dtype=torch.uint8, device=dev)
@@ -142,7 +132,7 @@ def main():
         else:
             b = mi.PktBatch(buf, n, offs=torch.from_numpy(offs.astype(np.int64)).to(dev),
                             lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()),
-                            packed=True, offs32=not args.offs64)
+                            packed=True, offs32=not offs64)
         mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r + 104729 * rank)
         mi.ipv4_finalize(b)  # TX path makes every packet valid
         batches.append(b)
@@ -150,12 +140,19 @@ def main():
                          l4=torch.empty(n, dtype=torch.uint16, device=dev),
                          status=torch.empty(n, dtype=torch.uint8, device=dev)))
     torch.cuda.synchronize()
-    # sanity: everything verifies
-    chk = mi.ipv4_verify(batches[0], bad_count=True)
+    chk = mi.ipv4_verify(batches[0], bad_count=True)  # sanity: everything verifies
     torch.cuda.synchronize()
     if int(chk["bad"].item()) != 0:
         raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
+    lay = (dict(stride=stride, first_off=first, fixed_len=L) if lens is None else dict(offs=offs, lens=lens))
+    return dict(batches=batches, outs=outs, n=n, L_sum=L_sum, cfg=cfg, scaling=scaling, lay=lay)
 
+
+def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_s: float = 0.0) -> dict:
+    """Warm up, then time exactly K verify passes over the rotating batches,
+    bracketed by a barrier + torch.cuda.synchronize() on both sides, max over
+    ranks.  Returns the config's value / ms_per_step / roofline (+ extras)."""
+    batches, outs, n, L_sum, cfg = wl["batches"], wl["outs"], wl["n"], wl["L_sum"], wl["cfg"]
     # The K passes are submitted by a prepared handle (mi_cksum_repeat_*: the
     # descriptors, kernel plans, streams and events are resolved once, as an RX
     # queue loop re-submitting its rings would), alternating over `nst`
@@ -195,13 +192,15 @@ def main():
     while time.perf_counter() - tw < args.settle:
         run(500, timed=True)
         settle_steps += 500
+    cfg = dict(cfg)
+    cfg["streams"] = nst
     cfg["settle_steps"] = settle_steps
     cfg["submit"] = ("graph" if use_graph else engine_note if engine_note else
                      f"prepared handle, AQL packets ({nst} own HSA queues)" if args.submit == "aql"
                      else "prepared handle, host launches")
     cfg["wait"] = args.wait
     if use_graph:  # instantiate the timed region's graph (K passes) before timing it
-        run(args.steps)
+        run(K)
 
     # The warmup ends with M untimed regions of K steps, bracketed exactly like
     # the timed one: the first region after the settle loop pays ~70-130 us of
@@ -212,21 +211,20 @@ def main():
         torch.cuda.synchronize()
         ta = time.perf_counter()
         if rep is not None:
-            rep.run(args.steps, timed=True)
+            rep.run(K, timed=True)
         else:
-            run(args.steps, timed=True)
+            run(K, timed=True)
         torch.cuda.synchronize()
         w = round((time.perf_counter() - ta) * 1e6, 1)
         warm_walls.append((w, round(rep.span(), 1)) if rep is not None else w)
 
     # ------------------------------------------------------- timed region
-    K = args.steps
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if rep is not None:
-        rep.run(K, timed=True)  # launches + hipEvents on the launch streams + wait
+        rep.run(K, timed=True)  # submission + completion events + wait
     else:
         span_us = run(K, timed=True)
     torch.cuda.synchronize()
@@ -250,16 +248,17 @@ def main():
 
     # Roofline of the dominant kernel (k_ipv4_verify*, the one verify_plan names).  Algorithmic bytes per
     # launch = sum(L) read + 5 B written per packet (ip u16, l4 u16, status u8).
-    # Average launch duration = GPU span of the timed region (hipEvents on the
-    # launch streams) / K: launches on different streams overlap, so this is the
-    # GPU time each launch costs; rocprof's union of dispatch intervals / K is
-    # the same quantity (tools/prof_summary.py).
+    # Average launch duration = GPU span of the timed region (dispatch
+    # timestamps of the handle's queues) / K: passes on different queues
+    # overlap, so this is the GPU time each launch costs; rocprof's union of
+    # dispatch intervals / K is the same quantity (tools/prof_summary.py).
     gpu_s_per_launch = span_us / K / 1e6
     alg_bytes = float(L_sum) + 5.0 * n
     achieved = alg_bytes / gpu_s_per_launch / 1e9
+    config = wl.get("name", args.config)
     traffic, tsrc = None, None
     tfile = os.path.join(ROOT, "profiles", "pmc_traffic_r02.json")
-    tkey = args.config + ("_u64" if args.offs64 else "_u32") if args.config == "pareto" else args.config
+    tkey = config + ("_u64" if args.offs64 else "_u32") if config == "pareto" else config
     if os.path.exists(tfile):
         try:
             ent = json.load(open(tfile)).get(tkey)
@@ -280,36 +279,109 @@ def main():
     iso_us, _ = mi.ipv4_verify_repeat(batches[:16], outs[:16], min(K, 100), nstreams=1, timing="pass")
     roof["isolated_launch_us"] = round(float(np.median(iso_us)), 2)
     roof["isolated_achieved"] = round(alg_bytes / (float(np.median(iso_us)) / 1e6) / 1e9, 1)
+    out = dict(value=round(value, 2), ms_per_step=round(elapsed / K * 1e3, 5), config=cfg,
+               mpkt_per_s=round(job_pkts / elapsed / 1e6, 2), roofline=roof, my_bytes=my_bytes,
+               my_elapsed=t1 - t0, job_pkts=job_pkts, elapsed=elapsed)
+    if warm_walls:
+        out["warm_region_walls_us"] = warm_walls
+    if trace:
+        out["host_trace_us"] = trace
+    if sustain_s > 0 and rep is not None:
+        # A sustained leg after the timed region (not part of `value`): the same
+        # handle re-run back to back for ~sustain_s seconds, so the GPU is busy
+        # long enough for an outside sampler to see it; its wall-clock rate
+        # corroborates the short region's.
+        torch.cuda.synchronize()
+        ts, passes, chunk = time.perf_counter(), 0, 2000
+        while time.perf_counter() - ts < sustain_s:
+            rep.run(chunk)
+            passes += chunk
+        torch.cuda.synchronize()
+        dts = time.perf_counter() - ts
+        out["sustained"] = dict(value=round(passes * L_sum / dts / GIB, 2), unit="GiB/s", passes=passes,
+                                seconds=round(dts, 2),
+                                frac_by_wall=round(passes * alg_bytes / dts / 1e9 / HBM_PEAK_GBS, 4),
+                                note="this rank, the same handle back to back after the timed region")
     if rep is not None:
         rep.close()
+    return out
 
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MI_BENCH_DEVICE / MI_BENCH_BACKEND exist only to rehearse the N>1 path on
+    # a one-GPU box (all ranks on one device, gloo); the driver's runs use
+    # LOCAL_RANK and RCCL ("nccl").
+    gpu = int(os.environ.get("MI_BENCH_DEVICE", local))
+    backend = os.environ.get("MI_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+
+    import libunsod_amd as mi
+    from libunsod_amd import shard, synth
+    if args.wait == "busy":
+        mi.set_busy_wait(True)
+
+    wl = build_workload(mi, synth, shard, args.config, args.rotate, args.offs64, dev, rank, world)
+    wl["name"] = args.config
+    K = args.steps
+    m = measure(mi, shard, wl, args, K, dev, dist, backend, sustain_s=args.sustain_seconds)
     result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": K,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / K * 1e3, 5), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "u8",
+        "metric": METRIC, "value": m["value"], "unit": "GiB/s", "n_gpus": world, "steps": K,
+        "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
+        "scaling": wl["scaling"], "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: device-generated IPv4/TCP datagrams (splitmix64 payload), TX-finalized to valid sums",
-        "config": cfg, "mpkt_per_s": round(job_pkts / elapsed / 1e6, 2), "roofline": roof,
+        "config": m["config"], "mpkt_per_s": m["mpkt_per_s"], "roofline": m["roofline"],
     }
-    if warm_walls:
-        result["warm_region_walls_us"] = warm_walls
-    if trace:
-        result["host_trace_us"] = trace
+    for k in ("warm_region_walls_us", "host_trace_us", "sustained"):
+        if k in m:
+            result[k] = m[k]
     if args.config == "64":
         # every 46 B datagram is one 64 B minimum Ethernet frame (14 B header +
         # 46 B + 4 B FCS): the frame-equivalent rate SURVEY.md 8(d) asks for
-        result["frame64_equiv_gibs"] = round(job_pkts * 64 / elapsed / GIB, 2)
+        result["frame64_equiv_gibs"] = round(m["job_pkts"] * 64 / m["elapsed"] / GIB, 2)
     if dist:
         # per-GPU rates (SURVEY.md 8(e) "Reporting"): timing bookkeeping only
-        mine = torch.tensor([my_bytes, t1 - t0], dtype=torch.float64,
+        mine = torch.tensor([m["my_bytes"], m["my_elapsed"]], dtype=torch.float64,
                             device=dev if backend == "nccl" else None)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         result["per_gpu"] = [round(float(x[0]) / float(x[1]) / GIB, 2) for x in allr]
 
     # -------------------------------------------- CPU baseline + host path
+    host = None
     if world == 1 and rank == 0:
-        host = batches[0].buf.cpu().numpy()
-        lay = dict(stride=stride, first_off=first, fixed_len=L) if lens is None else dict(offs=offs, lens=lens)
+        host = wl["batches"][0].buf.cpu().numpy()
+    n, L_sum, lay = wl["n"], wl["L_sum"], wl["lay"]
+    del wl, m
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+    # The metric names 1500 B AND 9000 B frames: the second frame size is timed
+    # in the same run, same K / W / submission, and reported beside the first.
+    if args.also and args.also != args.config:
+        wl2 = build_workload(mi, synth, shard, args.also, 0, args.offs64, dev, rank, world)
+        wl2["name"] = args.also
+        m2 = measure(mi, shard, wl2, args, K, dev, dist, backend)
+        result[f"config_{args.also}"] = dict(value=m2["value"], unit="GiB/s", ms_per_step=m2["ms_per_step"],
+                                             mpkt_per_s=m2["mpkt_per_s"], workload=m2["config"]["workload"],
+                                             rotating_batches=m2["config"]["rotating_batches"],
+                                             roofline=m2["roofline"])
+        del wl2
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+    if host is not None:
         if args.cpu_seconds > 0:
             result["cpu_baseline"] = cpu_baseline(host, n, L_sum, lay, args.cpu_seconds)
             result["cpu_baseline"]["plumbing_64k"] = plumbing_64k()

@@ -29,6 +29,8 @@
 
 #include <stdint.h>
 
+#include "mi_cksum_flags.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -287,10 +289,7 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b);
  *   anything else: no flags, csum_data = 0 (the stack computes as before).
  * Values are mbuf.h:281-305's.  csum_data may be NULL; bad_count as above.
  */
-#define MI_CSUM_IP_CHECKED 0x0100u
-#define MI_CSUM_IP_VALID   0x0200u
-#define MI_CSUM_DATA_VALID 0x0400u
-#define MI_CSUM_PSEUDO_HDR 0x0800u
+/* (MI_CSUM_IP_CHECKED / _IP_VALID / _DATA_VALID / _PSEUDO_HDR: mi_cksum_flags.h) */
 int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
                         uint32_t *bad_count, void *stream);
 
@@ -424,9 +423,7 @@ int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream);
  * [pkt_seg[i], pkt_seg[i+1]) and lands at dst + dst_first + i * dst_stride.
  * src, dst 16-byte aligned, both <= MI_BATCH_MAX_BYTES; l3_off <= 64.  status: n bytes.
  */
-#define MI_CSUM_IP  0x1u
-#define MI_CSUM_TCP 0x2u
-#define MI_CSUM_UDP 0x4u
+/* (MI_CSUM_IP / _TCP / _UDP: mi_cksum_flags.h) */
 #define MI_TX_NOBUFS     1u
 #define MI_TX_SHORT      2u
 #define MI_TX_NOSUM      4u

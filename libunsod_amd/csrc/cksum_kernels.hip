@@ -3220,34 +3220,39 @@ int aql_span(AqlRun *a, float *span_us) {
 // scope (the burst and the outputs live in host memory), a spin on the
 // completion signal.  Replaces a HIP launch + hipStreamSynchronize.
 //
-// Lifetime rule: every dispatch carries the completion signal, and nothing a
-// dispatch references (its kernel-argument slot, the scalar staging buffer,
-// the queue) is rewritten, freed or destroyed before that signal reads 0
-// (aql_one_quiesce).  A caller that returns on a result word the kernel
-// stores (the scalar drop-ins) does not wait for the signal itself; the next
-// call, a staging reallocation or the thread's exit does.
+// Lifetime rule: every dispatch carries the completion signal, which counts
+// the dispatches still outstanding (the host adds 1 per packet, the packet
+// processor subtracts 1 as each retires, in order: barrier bit).  Nothing a
+// dispatch references is rewritten, freed or destroyed before it has retired:
+// a kernel-argument slot is reused only once at most kAqlOneSlots - 1
+// dispatches are outstanding (so the one that used it last is done), and the
+// scalar staging buffer, the queue and the slots are freed only at 0
+// (aql_one_quiesce).  A caller that returns on a result word the kernel stores
+// (the scalar drop-ins) does not wait for its own dispatch to retire.
 struct AqlOne {
   int device = -1;
   AqlDevice *dev = nullptr;
   hsa_queue_t *q = nullptr;
-  hsa_signal_t sig{};
+  hsa_signal_t sig{};       // outstanding dispatches
   uint8_t *karg = nullptr;  // page-locked, mapped: kAqlOneSlots blocks of 512 B
   uint32_t next = 0;
-  bool inflight = false;    // a dispatch whose completion nobody has seen yet
+  bool inflight = false;    // dispatches may be outstanding
   std::atomic<int> err{0};  // the queue's error (aql_queue_error)
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
 
-// Wait (deadline-bounded) until the thread's last dispatch has retired.
-int aql_one_quiesce(AqlOne &o) {
+// Wait (deadline-bounded) until at most `left` of the thread's dispatches are
+// outstanding (0: all retired).
+int aql_one_quiesce(AqlOne &o, hsa_signal_value_t left = 0) {
   if (!o.inflight) return 0;
   const double t0 = mono_s();
-  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
+  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_LT, left + 1, 1000000, HSA_WAIT_STATE_ACTIVE) >
+         left) {
     if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
     if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
   }
-  o.inflight = false;
+  if (left == 0) o.inflight = false;
   return 0;
 }
 
@@ -3311,8 +3316,8 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
     o.device = t_ctx.device;
     thread_exit_register();
   }
-  // the previous dispatch must have retired before its resources are reused
-  int rc = aql_one_quiesce(o);
+  // the dispatch that last used the next argument slot must have retired
+  int rc = aql_one_quiesce(o, kAqlOneSlots - 1);
   if (rc) return rc;
   const AqlKernel &k = o.dev->k[id];
   if (k.kernarg > 512u) return set_err(-EPROTO, "AQL engine: kernarg segment %u B", k.kernarg);
@@ -3321,9 +3326,8 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   aql_fill_raw(ka, args, nargs, blocks, wg, k.kernarg);
   hsa_kernel_dispatch_packet_t t;
   aql_fill_packet(t, k, blocks, ka, wg);
-  hsa_signal_store_relaxed(o.sig, 1);
-  // one packet in flight at a time (quiesced above): the 64-entry queue always
-  // has room once the packet processor has consumed the previous ones
+  hsa_signal_add_relaxed(o.sig, 1);
+  // at most kAqlOneSlots packets outstanding (above): the 64-entry queue has room
   const uint64_t idx = hsa_queue_add_write_index_screlease(o.q, 1);
   const double t0 = mono_s();
   while (idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
@@ -4474,7 +4478,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
       bool retired;
       if (used_aql) {
         if (t_aql1.err.load()) return set_err(-EIO, "scalar fold: queue error 0x%x", t_aql1.err.load());
-        retired = hsa_signal_load_scacquire(t_aql1.sig) == 0;
+        retired = hsa_signal_load_scacquire(t_aql1.sig) == 0;  // ours is the latest
       } else {
         const hipError_t e = hipStreamQuery(c.sstream);
         if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));

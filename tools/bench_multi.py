@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--config", default="1500")
     ap.add_argument("--ms", default="1,2,4,8,16")
     ap.add_argument("--batches", type=int, default=320, help="batches verified per measurement")
+    ap.add_argument("--shapes", default="auto", help="lane-group shapes GxU to sweep (auto: the library's choice)")
     ap.add_argument("--caps", default="0", help="workgroup caps to sweep (0: the library default -- a resident-sized grid for "
                                                 "the multi-batch launch, 2048 for single launches)")
     a = ap.parse_args()
@@ -48,8 +49,10 @@ def main():
     torch.cuda.synchronize()
     s = torch.cuda.Stream()
     alg = n * L + 5 * n
-    for cap, m in [(c, m) for c in [int(x) for x in a.caps.split(",")] for m in [int(x) for x in a.ms.split(",")]]:
-        mi.set_shape(0, 0, cap)
+    shapes = [(0, 0) if x == "auto" else tuple(int(v) for v in x.split("x")) for x in a.shapes.split(",")]
+    for (g, u), cap, m in [(sh, c, m) for sh in shapes for c in [int(x) for x in a.caps.split(",")]
+                           for m in [int(x) for x in a.ms.split(",")]]:
+        mi.set_shape(g, u, cap)
         launches = a.batches // m
 
         def go(k):
@@ -71,7 +74,7 @@ def main():
             e1.record(s)
         s.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / (launches * m)
-        print(json.dumps(dict(config=a.config, batches_per_launch=m, launches=launches, streams=1, cap=cap or "default",
+        print(json.dumps(dict(config=a.config, shape=f"{g}x{u}" if g else "auto", batches_per_launch=m, launches=launches, streams=1, cap=cap or "default",
                               us_per_batch=round(us, 3), frac=round(alg / us / 8e6, 4),
                               GiBps=round(n * L / (us * 1e-6) / 2**30, 1))), flush=True)
 

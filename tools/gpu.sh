@@ -1,0 +1,78 @@
+#!/bin/bash
+# tools/gpu.sh STEP [STEP ...] -- the GPU-box steps of this repo, one script
+# instead of one-off files.  Every GPU step runs under its own time limit; the
+# chain stops at the first failure (exit status of that step).  Output goes to
+# gpurun_out/$TAG/ (TAG defaults to "run").
+#
+#   tests                 pytest -m gpu, the whole suite (-x, per-test timeout)
+#   tests:EXPR            pytest -m gpu -k EXPR
+#   smoke                 __graft_entry__.smoke()
+#   bench[:CFG[:ARGS]]    the driver's bench command (--steps 20 --warmup 5),
+#                         config CFG (1500 default); ARGS: extra bench.py flags,
+#                         comma-separated (e.g. bench:1500:--submit,launch)
+#   bench400[:CFG]        400 steps, no side legs
+#   prof[:CFG]            rocprofv3 --kernel-trace --stats of 400 steps with HIP
+#                         launches (the profiler serializes the AQL engine's
+#                         queues) + tools/prof_summary.py
+#   pmc:CFG:C1,C2,..      one rocprofv3 --pmc pass (counters only, 20 steps)
+#   py:SCRIPT[:ARGS]      python tools/SCRIPT with comma-separated ARGS, stdout
+#                         to $O/SCRIPT.jsonl
+#
+#   /usr/local/graft/bin/gpurun --timeout 900 -- 'TAG=r03x bash tools/gpu.sh tests smoke bench bench:9000'
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/${TAG:-run}
+mkdir -p "$O"
+
+fail() { echo "!! step '$1' failed (exit $2)"; exit "$2"; }
+
+for step in "$@"; do
+  IFS=: read -r kind a b <<< "$step"
+  extra=${b//,/ }
+  echo "== $step ($(date +%T))"
+  case $kind in
+    tests)
+      sel=(); [ -n "$a" ] && sel=(-k "$a")
+      timeout -k 10 700 python -u -m pytest tests -m gpu -x -v -s --timeout 180 --timeout-method thread "${sel[@]}" \
+        > "$O/gpu_tests${a:+_$a}.log" 2>&1 || fail "$step" $?
+      tail -1 "$O/gpu_tests${a:+_$a}.log" ;;
+    smoke)
+      timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || fail "$step" $?
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      cfg=${a:-1500}
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --config "$cfg" $extra \
+        > "$O/bench_$cfg.json" 2> "$O/bench_$cfg.err" || fail "$step" $?
+      cut -c1-400 "$O/bench_$cfg.json" ;;
+    bench400)
+      cfg=${a:-1500}
+      timeout -k 10 300 python -u bench.py --gpus 1 --steps 400 --warmup 5 --config "$cfg" --also none \
+        --sustain-seconds 0 --cpu-seconds 0 --no-host-path --no-dropin $extra \
+        > "$O/bench400_$cfg.json" 2>> "$O/bench400.err" || fail "$step" $?
+      cut -c1-300 "$O/bench400_$cfg.json" ;;
+    prof)
+      cfg=${a:-1500}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_$cfg" -o run --output-format csv -- \
+        python3 bench.py --steps 400 --warmup 5 --config "$cfg" --submit launch --also none --sustain-seconds 0 \
+        --cpu-seconds 0 --no-host-path --no-dropin > "$O/prof_$cfg.json" 2> "$O/prof_$cfg.err" || fail "$step" $?
+      f=$(ls "$O"/prof_"$cfg"/*/run_kernel_trace.csv "$O"/prof_"$cfg"/run_kernel_trace.csv 2>/dev/null | head -1)
+      python tools/prof_summary.py "$f" > "$O/prof_summary_$cfg.json" || fail "$step" $?
+      cut -c1-400 "$O/prof_summary_$cfg.json" ;;
+    pmc)
+      cfg=${a:-1500}
+      tag=$(echo "$b" | tr ',' '_' | cut -c1-40)
+      timeout -s KILL 120 rocprofv3 --pmc ${b//,/ } -d "$O/pmc_${cfg}_$tag" -o run --output-format csv -- \
+        python3 bench.py --steps 20 --warmup 5 --config "$cfg" --submit launch --also none --sustain-seconds 0 \
+        --settle 0 --warm-regions 0 --cpu-seconds 0 --no-host-path --no-dropin \
+        > "$O/pmc_${cfg}_$tag.json" 2> "$O/pmc_${cfg}_$tag.err" || fail "$step" $?
+      echo "pmc $cfg $b done" ;;
+    py)
+      scr=${a%.py}
+      timeout -k 10 600 python -u "tools/$scr.py" $extra > "$O/$scr.jsonl" 2> "$O/$scr.err" || fail "$step" $?
+      tail -3 "$O/$scr.jsonl" | cut -c1-300 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== all steps done ($(date +%T))"
