@@ -9,13 +9,13 @@
 #   smoke                 __graft_entry__.smoke()
 #   bench[:CFG[:ARGS]]    the driver's bench command (--steps 20 --warmup 5),
 #                         config CFG (1500 default); ARGS: extra bench.py flags,
-#                         comma-separated (e.g. bench:1500:--submit,launch)
+#                         '+' for spaces (e.g. bench:1500:--submit+launch)
 #   bench400[:CFG]        400 steps, no side legs
 #   prof[:CFG]            rocprofv3 --kernel-trace --stats of 400 steps with HIP
 #                         launches (the profiler serializes the AQL engine's
 #                         queues) + tools/prof_summary.py
 #   pmc:CFG:C1,C2,..      one rocprofv3 --pmc pass (counters only, 20 steps)
-#   py:SCRIPT[:ARGS]      python tools/SCRIPT with comma-separated ARGS, stdout
+#   py:SCRIPT[:ARGS]      python tools/SCRIPT with ARGS ('+' for spaces), stdout
 #                         to $O/SCRIPT.jsonl
 #
 #   /usr/local/graft/bin/gpurun --timeout 900 -- 'TAG=r03x bash tools/gpu.sh tests smoke bench bench:9000'
@@ -29,7 +29,7 @@ fail() { echo "!! step '$1' failed (exit $2)"; exit "$2"; }
 
 for step in "$@"; do
   IFS=: read -r kind a b <<< "$step"
-  extra=${b//,/ }
+  extra=${b//+/ }
   echo "== $step ($(date +%T))"
   case $kind in
     tests)
