@@ -1,7 +1,7 @@
-// libunsod_amd/csrc/cksum_device.h -- the device-side building blocks shared
-// by the library's kernel translation units (cksum_kernels.hip: the
-// lane-group / flat-run / slot / chain / TX kernels and the runtime;
-// stream_kernels.hip: the per-wave streaming verify): the fold arithmetic,
+// libunsod_amd/csrc/cksum_device.h -- the device-side building blocks of the
+// library's kernels (cksum_kernels.hip; kept apart so that an experimental
+// kernel can live in a translation unit of its own and compile in seconds):
+// the fold arithmetic,
 // the batch descriptor and its buffer resource, the IPv4 header parse, the
 // per-datagram RX verify results and their stores.  Internal; not part of
 // the C ABI.
@@ -607,8 +607,8 @@ __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uin
   }
 }
 
-// The kernel-argument table of a multi-batch launch (k_ipv4_verify_multi,
-// k_ipv4_verify_stream): up to kMaxMulti batches with their outputs.
+// The kernel-argument table of a multi-batch launch (k_ipv4_verify_multi):
+// up to kMaxMulti batches with their outputs.
 constexpr int kMaxMulti = 16;
 struct MultiEnt {
   Desc d;

@@ -47,8 +47,6 @@
 
 #include <algorithm>
 #include <atomic>
-#include <type_traits>
-#include <utility>
 #include <mutex>
 #include <vector>
 
@@ -2012,66 +2010,9 @@ unsigned slot64_blocks(const Desc &d) {
   return blocks ? (unsigned)blocks : 1u;
 }
 
-// The per-wave streaming kernel (k_ipv4_verify_stream) for lane-group plans:
-// MI_CKSUM_STREAM=1 (read per call) routes single verifies and multi-batch
-// launches through it.
-bool stream_on() {
-  const char *e = getenv("MI_CKSUM_STREAM");
-  return e && e[0] == '1';
-}
-// The stream kernel serves fixed-slot batches (no offset / length arrays),
-// except minimum-size frames in 64-byte slots (their slot kernel).
-bool stream_fits(const Desc &d) { return !d.offs && !d.lens; }
-bool stream_plan(const Desc &d, PlanKind k) {
-  return stream_fits(d) && (k == kPlanShape || (k == kPlanRun && !(d.flags & MI_BATCH_PACKED)));
-}
-// Resident grid of the stream kernel: occupancy x CUs, per device.
-uint64_t stream_resident() {
-  static std::atomic<uint64_t> res[64];
-  const int dv = t_ctx.device >= 0 && t_ctx.device < 64 ? t_ctx.device : 0;
-  uint64_t r = res[dv].load();
-  if (!r) {
-    const int per_cu = mi__stream_blocks_per_cu();
-    hipDeviceProp_t prop;
-    if (per_cu <= 0 || hipGetDeviceProperties(&prop, dv) != hipSuccess)
-      r = 2048;
-    else
-      r = (uint64_t)per_cu * (uint64_t)prop.multiProcessorCount;
-    res[dv].store(r);
-  }
-  return r;
-}
-// nb batches (their datagrams concatenated) in one stream launch.
-int launch_stream(const Desc *d, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4, uint8_t *const *st,
-                  uint32_t *bad, hipStream_t s) {
-  MultiArgs a{};
-  a.bad = bad;
-  uint64_t total = 0;
-  for (uint32_t k = 0; k < nb; ++k) {
-    a.e[k].d = d[k];
-    a.e[k].ip = ip ? ip[k] : nullptr;
-    a.e[k].l4 = l4 ? l4[k] : nullptr;
-    a.e[k].st = st ? st[k] : nullptr;
-    a.e[k].unit0 = (uint32_t)total;  // first datagram of batch k in the launch's numbering
-    total += d[k].n;
-    if (total > 0xffffffffull) return set_err(-E2BIG, "too many datagrams in one launch");
-  }
-  a.nb = nb;
-  a.units = (uint32_t)total;
-  if (!total) return 0;
-  uint64_t blocks = (total + (kBlock / 64) - 1) / (kBlock / 64);  // at least one datagram per wave
-  const uint64_t cap = g_tune.max_blocks > 0 ? (uint64_t)g_tune.max_blocks : stream_resident();
-  if (blocks > cap) blocks = cap;
-  const LaunchEv ev = t_lev;
-  t_lev = LaunchEv();
-  if (mi__stream_launch(&a, (unsigned)blocks, s, ev.start, ev.stop)) return launched();
-  return launched();
-}
-
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
   const Plan pl = verify_plan(d, max_len);
-  if (stream_on() && stream_plan(d, pl.kind) && !g_tune.g) return launch_stream(&d, 1, &ip, &l4, &st, bad, s);
   if (pl.kind == kPlanRun) {
     const dim3 grid(run_blocks(d));
     if (pl.run_u == 4)
@@ -2924,28 +2865,6 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
     ml = m > ml ? m : ml;
     merge = merge && verify_plan(d[k], m).kind == kPlanShape;
   }
-  if (stream_on() && !g_tune.g) {
-    // the lane-group / length-class batches in one stream launch, the
-    // flat-run / slot batches one launch each (same results)
-    Desc sd[kMaxMulti];
-    uint16_t *sip[kMaxMulti], *sl4[kMaxMulti];
-    uint8_t *sst[kMaxMulti];
-    uint32_t ns = 0;
-    for (uint32_t k = 0; k < nb; ++k) {
-      uint16_t *ipk = ip ? ip[k] : nullptr, *l4k = l4 ? l4[k] : nullptr;
-      uint8_t *stk = status ? status[k] : nullptr;
-      const PlanKind pk = verify_plan(d[k], batch_max_len(&b[k])).kind;
-      if (stream_plan(d[k], pk)) {
-        sd[ns] = d[k];
-        sip[ns] = ipk;
-        sl4[ns] = l4k;
-        sst[ns++] = stk;
-      } else if (d[k].n && (rc = launch_verify(d[k], batch_max_len(&b[k]), ipk, l4k, stk, bad_count, s))) {
-        return rc;
-      }
-    }
-    return ns ? launch_stream(sd, ns, sip, sl4, sst, bad_count, s) : 0;
-  }
   if (!merge) {  // flat-run / slot / length-class plans: one launch per batch (same results)
     for (uint32_t k = 0; k < nb; ++k)
       if (d[k].n && (rc = launch_verify(d[k], batch_max_len(&b[k]), ip ? ip[k] : nullptr, l4 ? l4[k] : nullptr,
@@ -2953,7 +2872,13 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
         return rc;
     return 0;
   }
-  const Shape sh = pick_shape(ml);
+  // One grid over several batches streams best with narrow groups and short
+  // passes (profiles/r03/shape_sweep_r03.jsonl, 16 x 1500 B batches per
+  // launch on one stream: 8x2 15.95 us per batch, 8x4 16.08, the single-launch
+  // choice 16x6 18.6); long datagrams keep pick_shape's.  A next-unit
+  // prefetch (two datagrams in flight per group) was measured slower: its
+  // registers cost a wave per SIMD (8x2 16.9, 8x4 16.3 us).
+  const Shape sh = g_tune.g ? pick_shape(ml) : ml <= 2019u ? Shape{8, 2} : pick_shape(ml);
   const uint32_t gpw = 64u / (uint32_t)sh.g;
   uint32_t units = 0;
   for (uint32_t k = 0; k < nb; ++k) {
@@ -3005,9 +2930,7 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
   Desc d;
   if (!b || make_desc(b, &d)) return "invalid batch";
   const Plan pl = verify_plan(d, batch_max_len(b));
-  if (stream_on() && stream_plan(d, pl.kind) && !g_tune.g)
-    snprintf(buf, sizeof buf, "k_ipv4_verify_stream<%d>", mi__stream_rows());
-  else if (pl.kind == kPlanRun)
+  if (pl.kind == kPlanRun)
     snprintf(buf, sizeof buf, "k_ipv4_verify_packed<%d>", pl.run_u);
   else if (pl.kind == kPlanShape)
     snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);

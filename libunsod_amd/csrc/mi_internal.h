@@ -25,14 +25,6 @@ uint8_t *mi__scalar_staging(size_t need);
 int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32_t src,
                     uint32_t dst, uint8_t proto, uint32_t plen, uint16_t *out);
 
-/* The per-wave streaming verify (stream_kernels.hip): `args` is a MultiArgs
- * kernel-argument table (cksum_device.h); launched on `stream` with optional
- * hipExtLaunchKernel timing events.  0 or -EIO. */
-int mi__stream_launch(const void *args, unsigned blocks, void *stream, void *ev_start, void *ev_stop);
-/* Resident blocks per CU of that kernel (-1 on error), and its ring depth. */
-int mi__stream_blocks_per_cu(void);
-int mi__stream_rows(void);
-
 /* Print "libmicksum: <what>: <last error>" and abort -- the (b1) drop-ins have
  * no error channel and no CPU fallback. */
 void mi__fatal(const char *what) __attribute__((noreturn));

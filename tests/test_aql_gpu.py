@@ -161,3 +161,32 @@ def test_aql_refuses_what_it_cannot_serve():
     b2, _ = _uniform(64, 1500, 2176, 142, 5, corrupt=False)
     with pytest.raises(mi.MiCksumError):
         mi.VerifyRepeat([b2], None, nstreams=1, op="finalize", engine="aql")
+
+
+@pytest.mark.parametrize("nq", [2, 4])
+def test_aql_rewritten_batches_between_runs(nq):
+    """every queue's first packet acquires at system scope, so a
+    run sees batch bytes rewritten between runs (a re-filled RX ring: here a
+    host-to-device copy of different datagrams into the same buffers) on
+    every queue, not stale lines of the previous run.  The outputs are checked
+    after each run against the oracle of the bytes the run saw."""
+    n, L, stride, first = 4096, 1500, 2176, 142
+    nb = 2 * nq
+    gens = [[_uniform(n, L, stride, first, 900 + 17 * g + r) for r in range(nb)] for g in range(3)]
+    bs = [b for b, _ in gens[0]]
+    outs = [_outs(n) for _ in bs]
+    torch.cuda.synchronize()
+    rep = mi.VerifyRepeat(bs, outs, nstreams=nq, engine="aql")
+    try:
+        for g in range(3):
+            if g:
+                for b, (bg, _) in zip(bs, gens[g]):
+                    b.buf.copy_(bg.buf)  # new datagrams into the same device buffers
+                for o in outs:
+                    for t in o.values():
+                        t.fill_(0xEE)
+                torch.cuda.synchronize()
+            rep.run(nb)  # one pass over every batch, spread over the nq queues
+            _check(outs, [w for _, w in gens[g]])
+    finally:
+        rep.close()
