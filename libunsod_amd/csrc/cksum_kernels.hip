@@ -2066,15 +2066,16 @@ int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd
 // header blocks -- the 64-byte blocks from off - a up to the last one a field
 // can reach (off + 77: hl 60 + TCP sum 16 + 1) -- hold no other datagram's
 // byte: the previous datagram ends by off - a, the next starts after them.
-// Off by default, MI_CKSUM_TX_BLOCKS=1 turns the whole-block stores on: on
-// MI355X they measured no faster than the byte stores (1500 B 36.4 vs 34.5 us,
-// 9000 B 100.7 vs 97.9 us, profiles/finalize_r02.jsonl), and a bare read +
-// 64 B-block store probe costs the same as read + 4 B store
-// (profiles/ceiling_writes_r02.jsonl): the price is the scattered write, not
-// its width.
+// On by default (MI_CKSUM_TX_BLOCKS=0: byte stores).  Both schemes leave the
+// L2 as one 64-byte write per datagram (TCC_EA0_WRREQ_64B = 65536 per 1500 B
+// batch, profiles/r03/finalize_r03.jsonl); the byte stores' write carries a
+// partial byte mask, which the memory side completes by read-modify-write,
+// the whole block does not: 1500 B 19.0 -> 17.4 us, 9000 B 97.5 -> 96.0 us
+// on the same box.  (Round 2 measured the opposite order on another box with
+// the round-2 BLOCKS kernel, whose deferred-store state sat in scratch.)
 bool finalize_blocks_ok(const Desc &d, uint32_t max_len) {
   const char *e = getenv("MI_CKSUM_TX_BLOCKS");  // per launch, so tests can switch it
-  const bool allow = e && e[0] == '1';
+  const bool allow = !(e && e[0] == '0');
   constexpr uint64_t B = MI_TX_BLOCK;
   if (!allow || d.offs || !d.stride || d.stride % B || !max_len) return false;
   const uint64_t a = d.first_off % B;

@@ -5,7 +5,7 @@ prepared handle, K back-to-back passes alternating over 2 streams, R rotating
 batches with >= 2 GiB read between two uses of one).  One JSON line per
 (config, op): GPU span per pass, algorithmic bytes = datagram bytes read + the
 op's bytes written (finalize: 4 B, verify: 5 B per datagram), fraction of the
-8 TB/s spec peak.  MI_CKSUM_TX_BLOCKS=1 selects the whole-block finalize stores (A/B).
+8 TB/s spec peak.  MI_CKSUM_TX_BLOCKS=0 selects the byte-store finalize (A/B).
 
     python tools/bench_finalize.py [--configs 1500,9000,pareto,64] [--steps 400]
 """
@@ -65,7 +65,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    blocks = os.environ.get("MI_CKSUM_TX_BLOCKS", "0") == "1"
+    blocks = os.environ.get("MI_CKSUM_TX_BLOCKS", "1") != "0"
     for cfg in a.configs.split(","):
         bs, n, lsum = make_batches(cfg, dev)
         outs = [dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),

@@ -17,6 +17,8 @@
 #   pmc:CFG:C1,C2,..      one rocprofv3 --pmc pass (counters only, 20 steps)
 #   py:SCRIPT[:ARGS]      python tools/SCRIPT with ARGS ('+' for spaces), stdout
 #                         to $O/SCRIPT.jsonl
+#   pmcpy:SCRIPT:C1,C2,..[:ARGS]  one rocprofv3 --pmc pass over python tools/SCRIPT
+#   host                  the box's identity (hostname, GPU serial, driver, clocks)
 #
 #   /usr/local/graft/bin/gpurun --timeout 900 -- 'TAG=r03x bash tools/gpu.sh tests smoke bench bench:9000'
 set -o pipefail
@@ -28,7 +30,7 @@ mkdir -p "$O"
 fail() { echo "!! step '$1' failed (exit $2)"; exit "$2"; }
 
 for step in "$@"; do
-  IFS=: read -r kind a b <<< "$step"
+  IFS=: read -r kind a b c <<< "$step"
   extra=${b//+/ }
   echo "== $step ($(date +%T))"
   case $kind in
@@ -71,6 +73,16 @@ for step in "$@"; do
       scr=${a%.py}
       timeout -k 10 600 python -u "tools/$scr.py" $extra > "$O/$scr.jsonl" 2> "$O/$scr.err" || fail "$step" $?
       tail -3 "$O/$scr.jsonl" | cut -c1-300 ;;
+    pmcpy)
+      scr=${a%.py}
+      tag=$(echo "$b" | tr ',' '_' | cut -c1-60)
+      timeout -s KILL 180 rocprofv3 --pmc ${b//,/ } -d "$O/pmc_${scr}_$tag" -o run --output-format csv -- \
+        python3 "tools/$scr.py" ${c//+/ } > "$O/pmc_${scr}_$tag.out" 2> "$O/pmc_${scr}_$tag.err" || fail "$step" $?
+      echo "pmc $scr $b done" ;;
+    host)
+      { hostname; cat /sys/class/drm/card*/device/serial_number 2>/dev/null | head -8; rocm-smi --showproductname \
+        --showserial --showmeminfo vram 2>/dev/null | grep -v "^$" | head -30; } > "$O/host.txt" 2>&1 || true
+      head -3 "$O/host.txt" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
