@@ -2619,39 +2619,70 @@ int aql_span(AqlRun *a, float *span_us) {
 // scope (the burst and the outputs live in host memory), a spin on the
 // completion signal.  Replaces a HIP launch + hipStreamSynchronize.
 //
-// Lifetime rule: every dispatch carries the completion signal, which counts
-// the dispatches still outstanding (the host adds 1 per packet, the packet
-// processor subtracts 1 as each retires, in order: barrier bit).  Nothing a
-// dispatch references is rewritten, freed or destroyed before it has retired:
-// a kernel-argument slot is reused only once at most kAqlOneSlots - 1
-// dispatches are outstanding (so the one that used it last is done), and the
-// scalar staging buffer, the queue and the slots are freed only at 0
-// (aql_one_quiesce).  A caller that returns on a result word the kernel stores
-// (the scalar drop-ins) does not wait for its own dispatch to retire.
+// Lifetime rule: nothing a dispatch references (its kernel-argument slot, the
+// scalar staging buffer, the queue) is rewritten, freed or destroyed before
+// the dispatch is done with it.
+//  * wait = true (host bursts): the packet carries the completion signal and
+//    the call spins on it -- retired on return.
+//  * wait = false (the (b1) drop-ins): no completion signal (a signal costs
+//    its completion event on every call, ~1.5 us, profiles/r03); the caller
+//    spins on the result word the kernel stores as its last action, after
+//    every read of its arguments and of the staging buffer -- so the next call
+//    may rewrite both, and a slot is reused only kAqlOneSlots calls later.
+//    Before the staging buffer is freed or the queue destroyed,
+//    aql_one_quiesce appends a barrier-AND packet with the signal: it
+//    completes once every earlier packet has retired.
 struct AqlOne {
   int device = -1;
   AqlDevice *dev = nullptr;
   hsa_queue_t *q = nullptr;
-  hsa_signal_t sig{};       // outstanding dispatches
+  hsa_signal_t sig{};
   uint8_t *karg = nullptr;  // page-locked, mapped: kAqlOneSlots blocks of 512 B
   uint32_t next = 0;
-  bool inflight = false;    // dispatches may be outstanding
+  bool unretired = false;   // unsignalled dispatches whose retirement nobody has seen
   std::atomic<int> err{0};  // the queue's error (aql_queue_error)
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
 
-// Wait (deadline-bounded) until at most `left` of the thread's dispatches are
-// outstanding (0: all retired).
-int aql_one_quiesce(AqlOne &o, hsa_signal_value_t left = 0) {
-  if (!o.inflight) return 0;
+// Reserve the next packet slot of the thread's queue (deadline-bounded).
+int aql_one_slot(AqlOne &o, uint64_t *idx, void **slot) {
+  *idx = hsa_queue_add_write_index_screlease(o.q, 1);
   const double t0 = mono_s();
-  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_LT, left + 1, 1000000, HSA_WAIT_STATE_ACTIVE) >
-         left) {
+  while (*idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
+    if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
+    if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: queue full for 10 s");
+  }
+  *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (*idx & (o.q->size - 1));
+  return 0;
+}
+// Spin (deadline-bounded) until the signal reads 0.
+int aql_one_wait(AqlOne &o) {
+  const double t0 = mono_s();
+  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
     if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
     if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
   }
-  if (left == 0) o.inflight = false;
+  return 0;
+}
+// Every packet of the thread's queue retired (a barrier-AND packet behind them).
+int aql_one_quiesce(AqlOne &o) {
+  if (!o.unretired) return 0;
+  uint64_t idx;
+  void *p;
+  int rc = aql_one_slot(o, &idx, &p);
+  if (rc) return rc;
+  hsa_barrier_and_packet_t *bp = (hsa_barrier_and_packet_t *)p;
+  memset((uint8_t *)bp + 4, 0, sizeof *bp - 4);
+  bp->completion_signal = o.sig;
+  hsa_signal_store_relaxed(o.sig, 1);
+  const uint32_t sc = HSA_FENCE_SCOPE_SYSTEM;
+  const uint32_t hs = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
+                      (sc << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (sc << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
+  __atomic_store_n((uint32_t *)bp, hs, __ATOMIC_RELEASE);
+  hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
+  if ((rc = aql_one_wait(o))) return rc;
+  o.unretired = false;
   return 0;
 }
 
@@ -2669,7 +2700,7 @@ void aql_one_release(AqlOne &o) {
   o.sig = hsa_signal_t{};
   o.karg = nullptr;
   o.next = 0;
-  o.inflight = false;
+  o.unretired = false;
   o.err.store(0);
 }
 
@@ -2715,9 +2746,6 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
     o.device = t_ctx.device;
     thread_exit_register();
   }
-  // the dispatch that last used the next argument slot must have retired
-  int rc = aql_one_quiesce(o, kAqlOneSlots - 1);
-  if (rc) return rc;
   const AqlKernel &k = o.dev->k[id];
   if (k.kernarg > 512u) return set_err(-EPROTO, "AQL engine: kernarg segment %u B", k.kernarg);
   uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
@@ -2725,17 +2753,14 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   aql_fill_raw(ka, args, nargs, blocks, wg, k.kernarg);
   hsa_kernel_dispatch_packet_t t;
   aql_fill_packet(t, k, blocks, ka, wg);
-  hsa_signal_add_relaxed(o.sig, 1);
-  // at most kAqlOneSlots packets outstanding (above): the 64-entry queue has room
-  const uint64_t idx = hsa_queue_add_write_index_screlease(o.q, 1);
-  const double t0 = mono_s();
-  while (idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
-    if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
-    if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: queue full for 10 s");
-  }
-  hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (idx & (o.q->size - 1));
+  uint64_t idx;
+  void *p;
+  int rc = aql_one_slot(o, &idx, &p);
+  if (rc) return rc;
+  hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)p;
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
-  slot->completion_signal = o.sig;
+  if (wait) hsa_signal_store_relaxed(o.sig, 1);
+  slot->completion_signal = wait ? o.sig : hsa_signal_t{0};
   // system-scope fences both ways: the kernels read host memory the host
   // rewrites every call (burst, staging, descriptors) and write host memory
   const uint32_t sc = HSA_FENCE_SCOPE_SYSTEM;
@@ -2743,10 +2768,12 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
                       (sc << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (sc << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) |
                       ((uint32_t)t.setup << 16);
   __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
-  o.inflight = true;
   hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
-  if (!wait) return 0;
-  return aql_one_quiesce(o);
+  if (!wait) {
+    o.unretired = true;
+    return 0;
+  }
+  return aql_one_wait(o);
 }
 
 }  // namespace
@@ -3797,7 +3824,7 @@ uint8_t *mi__scalar_staging(size_t need) {
   if (c.stage_cap < need) {
     // the thread's last scalar dispatch may still be retiring: it must be done
     // with the old buffer before it is freed
-    if (t_aql1.inflight && aql_one_quiesce(t_aql1)) return nullptr;
+    if (aql_one_quiesce(t_aql1)) return nullptr;
     if (c.sstream && hipStreamSynchronize(c.sstream) != hipSuccess) {
       set_err(-EIO, "scalar staging: stream");
       return nullptr;
@@ -3880,10 +3907,9 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     if ((polls & 255u) == 0) {
       // has the dispatch ended without the word?  (re-read after: the store
       // and the completion race)
-      bool retired;
+      bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
       if (used_aql) {
         if (t_aql1.err.load()) return set_err(-EIO, "scalar fold: queue error 0x%x", t_aql1.err.load());
-        retired = hsa_signal_load_scacquire(t_aql1.sig) == 0;  // ours is the latest
       } else {
         const hipError_t e = hipStreamQuery(c.sstream);
         if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));
