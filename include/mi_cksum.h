@@ -100,6 +100,14 @@ int mi_cksum_hsa_queues(void);
  * `max_blocks` workgroups.  0, 0, 0 restores the automatic choice.  Shapes
  * change speed only, never results.  -EINVAL for a shape not compiled in. */
 int mi_cksum_set_shape(int group, int chunks, int max_blocks);
+/* Tuning knob (process-wide): the flat-run kernel that verifies packed
+ * batches with an offset array -- `chunks` = 0: the register-streaming one
+ * (k_ipv4_verify_packed, the default); otherwise the LDS-DMA one
+ * (k_ipv4_verify_run_dma) with `chunks` 16-byte chunks per lane per pass and
+ * a ring of `slots` passes per wave (2x3, 2x4, 4x2, 4x3 are compiled in;
+ * MI_CKSUM_RUN_DMA=UxR sets the initial choice).  Speed only, never results.
+ * -EINVAL for a shape not compiled in. */
+int mi_cksum_set_run_kernel(int chunks, int slots);
 
 /* ------------------------------------------------------------------------ */
 /* (b2) batch offload                                                         */

@@ -9,7 +9,7 @@ from ._lib import (LIB_PATH, MI_SPAN_ABS, MI_SPAN_STREAM, MI_ST_IP_BAD, MI_ST_L4
                    MiCksumError, load)
 from .api import (ChainBatch, MbufChain, chain_batch, PktBatch, device_count, host_register, host_unregister, in_addword, in_cksum,
                   in_cksum_hdr, in_cksum_pseudo_header, in_cksum_skip, in_pseudo, init, ipv4_finalize,
-                  ipv4_verify, ipv4_verify_multi, ipv4_verify_host, rx_offload_host, ipv4_verify_repeat, VerifyRepeat, rx_offload, set_busy_wait, set_shape, verify_plan, span_batch, synth_ipv4, version,
+                  ipv4_verify, ipv4_verify_multi, ipv4_verify_host, rx_offload_host, ipv4_verify_repeat, VerifyRepeat, rx_offload, set_busy_wait, set_shape, set_run_kernel, verify_plan, span_batch, synth_ipv4, version,
                   TxBatch, tx_copy)
 
 load()

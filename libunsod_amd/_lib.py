@@ -130,6 +130,7 @@ SIGNATURES = {
     "mi_cksum_strerror": (C.c_char_p, []),
     "mi_cksum_version": (C.c_char_p, []),
     "mi_cksum_set_shape": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    "mi_cksum_set_run_kernel": (C.c_int, [C.c_int, C.c_int]),
     "mi_cksum_span_batch": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(SpanSeedsC), C.c_void_p,
                                       C.c_void_p]),
     "mi_cksum_chain_batch": (C.c_int, [C.POINTER(ChainBatchC), C.c_void_p, C.c_void_p]),

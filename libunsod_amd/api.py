@@ -498,6 +498,12 @@ def set_shape(group: int = 0, chunks: int = 0, max_blocks: int = 0) -> None:
     check("mi_cksum_set_shape", load().mi_cksum_set_shape(group, chunks, max_blocks))
 
 
+def set_run_kernel(chunks: int = 0, slots: int = 0) -> None:
+    """Flat-run kernel for packed batches: 0 = register streaming (default),
+    else the LDS-DMA kernel with `chunks` x `slots` (mi_cksum_set_run_kernel)."""
+    check("mi_cksum_set_run_kernel", load().mi_cksum_set_run_kernel(chunks, slots))
+
+
 def init(device: int = 0) -> None:
     check("mi_cksum_init", load().mi_cksum_init(device))
 
@@ -513,6 +519,6 @@ def version() -> str:
 __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
-    "ipv4_verify_host", "ipv4_verify_multi", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_busy_wait", "init", "device_count", "version",
+    "ipv4_verify_host", "ipv4_verify_multi", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_run_kernel", "set_busy_wait", "init", "device_count", "version",
     "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
 ]

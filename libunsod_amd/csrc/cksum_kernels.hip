@@ -517,6 +517,310 @@ __global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uin
   packed_body<U, MODE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
 
+// The bounds of a wave's 64-datagram range (the flat-run kernels): the run
+// [r0, r0 + 16 nch) of chunks it streams, and whether it is compact enough.
+struct RunRange {
+  uint32_t r0 = 0, nch = 0;
+  bool packed = false;
+};
+template <int SPAN>
+__device__ __forceinline__ RunRange run_range(const Desc &d, uint32_t p0, uint32_t lane, uint32_t off,
+                                              uint32_t flen) {
+  RunRange rr;
+  const bool act = p0 + lane < d.n;
+  const uint32_t end = act ? off + flen : 0u;
+  const bool sane = !act || (off < kOOB && end >= off && end <= d.bytes && (!SPAN || flen <= 65535u));
+  rr.r0 = wave_min(act ? off : ~0u) & ~15u;
+  const uint32_t r1 = wave_max(end);
+  rr.nch = (r1 - rr.r0 + 15u) >> 4;
+  const uint32_t dbytes = wave_total(act ? min(flen, 0xffffu) : 0u);
+  rr.packed = p0 < d.n && __all(sane) && (uint64_t)rr.nch * 16u <= 2ull * dbytes + 4096u;
+  return rr;
+}
+
+// RX verify of a PACKED batch through LDS-DMA (round 3; the flat run of
+// k_ipv4_verify_packed with its loads moved off the register file).
+//
+// The flat-run kernel keeps a pass of the run in VGPRs, so a wave has bytes in
+// flight only between issuing a pass and scanning it: per range it waits out
+// the descriptor loads, each pass and the per-datagram work in turn, and the
+// pass registers (plus the header state) hold it at 16 waves per CU.  Here
+// every byte the stream reads lands in LDS by `buffer_load_dwordx4 ... lds`
+// (no VGPR destination): each wave owns a ring of R pass slots (64*U chunks
+// each) and keeps up to R-1 passes in flight while it scans one -- across
+// range boundaries, so the next range's first passes stream in while this
+// range's datagrams are parsed and their verdicts stored.  The descriptors
+// (offsets, lengths) come in the same way, one range ahead.
+//
+// Ordering (the LDS-DMA rules of MI355X_MICROARCH.md item 7): nothing orders a
+// ds_read behind a pending DMA except the issuing wave's covering vmcnt, so the
+// wave counts: `gi` passes issued, `gc` the pass being scanned; the gi-gc-1
+// passes issued after it are the youngest U*(gi-gc-1) of the wave's vector
+// memory operations it can be sure of (stores, atomics and descriptor DMAs in
+// between only add to that), and `s_waitcnt vmcnt(U*(gi-gc-1))` retires pass gc
+// (wait_vm_ladder: the immediate comes from a uniform branch ladder).  A
+// slot is refilled only after lgkmcnt(0) has retired the reads of its last scan.
+// Only this wave reads its slots, so no barrier is involved.
+#ifndef MI_RUN_DMA_U
+#define MI_RUN_DMA_U 2
+#endif
+#ifndef MI_RUN_DMA_R
+#define MI_RUN_DMA_R 4
+#endif
+// the instantiated shapes (U, R)
+#define MI_RUN_DMA_SHAPES(X) X(2, 3) X(2, 4) X(4, 2) X(4, 3)
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8])
+constexpr int waitcnt_vm(int n) { return (n & 15) | (((n >> 4) & 3) << 14) | (7 << 4) | (15 << 8); }
+constexpr int kWaitLgkm0 = 15 | (3 << 14) | (7 << 4);
+template <int U, int K>
+__device__ __forceinline__ void wait_vm_ladder(uint32_t k) {  // vmcnt(U * min(k, K)), k wave-uniform
+  if constexpr (K == 0) {
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  } else {
+    if (k >= (uint32_t)K)
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(U * K));
+    else
+      wait_vm_ladder<U, K - 1>(k);
+  }
+}
+// LDS reads of the DMA kernel are inline asm, each group closed by its own
+// lgkmcnt(0): the compiler treats a plain LDS read as a possible reader of
+// every pending LDS-DMA and puts a vmcnt(0) -- a drained ring -- in front of
+// it.  The kernel's own counted vmcnt waits order what does depend on a DMA.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ uint32_t lds_rd32(const void *p) {
+  uint32_t x;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(p)) : "memory");
+  return x;
+}
+template <int U, int R>
+__device__ __forceinline__ void run_dma_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                             uint32_t *bad) {
+  constexpr uint32_t W = 64u * U;  // chunks per pass
+  constexpr int NW = kBlock / 64;
+  __shared__ u32x4 s_ring[NW][R][W];
+  __shared__ uint32_t s_q[NW][W];
+  __shared__ uint32_t s_desc[NW][192];  // [0, 64) offset (low dword), [64, 128) high dword, [128, 192) length
+  typedef __attribute__((address_space(3))) void *lds_ptr;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const bool o32 = d.flags & MI_BATCH_OFFS32;
+  const uint64_t obytes = (uint64_t)d.n * (o32 ? 4u : 8u), lbytes = d.lens ? (uint64_t)d.n * 4u : 0u;
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint64_t *>(d.offs), 0, (int)(obytes < kOOB ? obytes : kOOB), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      d.lens ? (void *)const_cast<uint32_t *>(d.lens) : (void *)const_cast<uint64_t *>(d.offs), 0,
+      (int)(lbytes < kOOB ? lbytes : kOOB), 0x00020000);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t rstride = gridDim.x * NW * 64u;
+  uint32_t *sq = s_q[wv];
+  uint32_t p0 = (blockIdx.x * NW + wv) * 64u;
+  if (p0 >= d.n) return;
+  // the 64 descriptors of the range at p into s_desc (three DMAs)
+  auto desc_dma = [&](uint32_t p) {
+    const bool in = p + lane < d.n;
+    const uint32_t lo = in ? (o32 ? 4u : 8u) * (p + lane) : kOOB;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr)&s_desc[wv][0], 4, lo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr)&s_desc[wv][64], 4, in && !o32 ? lo + 4u : kOOB, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rl, (lds_ptr)&s_desc[wv][128], 4, in ? 4u * (p + lane) : kOOB, 0, 0, 0);
+  };
+  // this lane's datagram of the range at p, from s_desc (pkt_off / pkt_len)
+  auto desc_read = [&](uint32_t p, uint32_t &o, uint32_t &l) {
+    o = 0;
+    l = 0;
+    if (p + lane < d.n) {
+      const uint32_t lo = lds_rd32(&s_desc[wv][lane]), hi = o32 ? 0u : lds_rd32(&s_desc[wv][64u + lane]);
+      o = hi || lo >= kOOB ? kOOB : lo;
+      const uint32_t x = d.lens ? lds_rd32(&s_desc[wv][128u + lane]) : d.fixed_len;
+      l = x < 0x7fff0000u ? x : 0x7fff0000u;
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);  // read before the next descriptor DMA rewrites them
+  };
+  auto passes = [&](const RunRange &q) { return q.packed ? (q.nch + W - 1u) / W : 0u; };
+
+  // current range (p0, off, flen, rr, P), next range (pn, offn, flenn, rn, Pn)
+  desc_dma(p0);
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+  uint32_t off, flen;
+  desc_read(p0, off, flen);
+  RunRange rr = run_range<0>(d, p0, lane, off, flen);
+  uint32_t P = passes(rr);
+  uint32_t pn = p0 + rstride;
+  desc_dma(pn);  // out-of-range lanes fetch nothing
+  uint32_t gi_desc = 0;  // passes issued when the pending descriptor DMA went out
+  uint32_t offn = 0, flenn = 0, Pn = 0;
+  RunRange rn;
+  // the issuer: in the current range (nxt = false) or the next one
+  bool nxt = false;
+  uint32_t ip = 0, gi = 0, gc = 0;
+  auto issue_pass = [&](const RunRange &q, uint32_t k) {
+    u32x4 *slot = s_ring[wv][gi % R];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t c = k * W + 64u * u + lane;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr)(slot + 64u * u), 16, c < q.nch ? q.r0 + 16u * c : kOOB, 0,
+                                              0, 2);
+    }
+    ++gi;
+  };
+  // the issuer moves on to the next range: its descriptors (DMA'd a range
+  // ago), its bounds, and the DMA of the descriptors of the range after it
+  auto cross = [&]() {
+    if (pn < d.n) {
+      wait_vm_ladder<U, R - 1>((uint32_t)__builtin_amdgcn_readfirstlane((int)(gi - gi_desc)));
+      desc_read(pn, offn, flenn);
+      rn = run_range<0>(d, pn, lane, offn, flenn);
+      Pn = passes(rn);
+      desc_dma(pn + rstride);
+      gi_desc = gi;
+    } else {
+      Pn = 0;
+    }
+    nxt = true;
+    ip = 0;
+  };
+  auto issue_next = [&]() {
+    if (gi - gc >= (uint32_t)R) return;  // every slot holds an unscanned pass
+    if (!nxt && ip < P) {
+      issue_pass(rr, ip++);
+      return;
+    }
+    if (!nxt) cross();
+    if (ip < Pn) issue_pass(rn, ip++);
+  };
+  for (int j = 0; j < R - 1; ++j) issue_next();
+
+  for (;;) {
+    const uint32_t i = p0 + lane;
+    const bool act = i < d.n;
+    const uint32_t end = act ? off + flen : 0u;
+    const uint32_t st = act ? off - rr.r0 : 0u, en = act ? end - rr.r0 : 0u;
+    const uint32_t cs = st >> 4, ce = en >> 4, h = st & 15u, t = en & 15u;
+    u32x4 hv[3], tv;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) hv[k] = u32x4{0, 0, 0, 0};
+    tv = u32x4{0, 0, 0, 0};
+    uint32_t carry = 0, qs = 0, qe = 0;
+    for (uint32_t cp = 0; cp < P; ++cp) {
+      issue_next();
+      wait_vm_ladder<U, R - 1>((uint32_t)__builtin_amdgcn_readfirstlane((int)(gi - gc - 1u)));  // pass gc has landed
+      const u32x4 *slot = s_ring[wv][gc % R];
+      const uint32_t cb = cp * W;
+      u32x4 v[U];
+      if constexpr (U == 2) {
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:1024\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(v[0]), "=&v"(v[1])
+                     : "v"(lds_addr(&slot[lane]))
+                     : "memory");
+      } else {
+        static_assert(U == 4, "U");
+        asm volatile(
+            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1024\n\tds_read_b128 %2, %4 offset:2048\n\t"
+            "ds_read_b128 %3, %4 offset:3072\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+            : "v"(lds_addr(&slot[lane]))
+            : "memory");
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t x = cb + 64u * u + lane < rr.nch ? sum4(v[u]) : 0u;
+        const uint32_t inc = wave_scan(x);
+        sq[64u * u + lane] = carry + inc - x;
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      {
+        // this pass's lookups, read unconditionally (index 0 when not needed)
+        // and kept where they apply
+        const bool ins = cs - cb < W, ine = ce - cb < W;
+        bool inh[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) inh[k] = act && cs + k - cb < W && cs + k < rr.nch;
+        const bool intv = act && t && ine;
+        uint32_t q0, q1;
+        u32x4 x0, x1, x2, x3;
+        asm volatile(
+            "ds_read_b32 %0, %6\n\tds_read_b32 %1, %7\n\tds_read_b128 %2, %8\n\tds_read_b128 %3, %9\n\t"
+            "ds_read_b128 %4, %10\n\tds_read_b128 %5, %11\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(q0), "=&v"(q1), "=&v"(x0), "=&v"(x1), "=&v"(x2), "=&v"(x3)
+            : "v"(lds_addr(&sq[ins ? cs - cb : 0u])), "v"(lds_addr(&sq[ine ? ce - cb : 0u])),
+              "v"(lds_addr(&slot[inh[0] ? cs - cb : 0u])), "v"(lds_addr(&slot[inh[1] ? cs + 1u - cb : 0u])),
+              "v"(lds_addr(&slot[inh[2] ? cs + 2u - cb : 0u])), "v"(lds_addr(&slot[intv ? ce - cb : 0u]))
+            : "memory");
+        qs = ins ? q0 : qs;
+        qe = ine ? q1 : qe;
+        hv[0] = inh[0] ? x0 : hv[0];
+        hv[1] = inh[1] ? x1 : hv[1];
+        hv[2] = inh[2] ? x2 : hv[2];
+        tv = intv ? x3 : tv;
+      }
+      // the slot's reads and the s_q lookups are done before it is refilled
+      // (the next issue_next) or s_q is rewritten
+      __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+      __builtin_amdgcn_wave_barrier();
+      ++gc;
+    }
+    if (!rr.packed) {
+      // not packed: one lane per datagram (ordinary loads)
+      if (act) {
+        u32x4 w[4];
+        issue_first<1, 4>(r, off, flen, 0, w);
+        IpHdr ih;
+        bool hdr_ok, l4_ok;
+        uint32_t sum_h, sum_l;
+        const bool demux = d.flags & MI_BATCH_DEMUX;
+        ipv4_sums<1, 4, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l, demux);
+        verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
+                    ip_out, l4_out, st_out, bad, d);
+      }
+    } else if (act) {
+      if (ce >= rr.nch) qe = carry;  // end on the run's last chunk boundary
+      const IpHdr ih = parse_ipv4<1, 3>(hv, h);
+      const bool odd = h & 1u;
+      const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
+      const bool l4_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
+      const uint32_t hend = hdr_ok ? ih.hl : 0u;
+      const uint32_t lend = l4_ok ? ih.iplen : hend;
+      uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(hv[0], 0, 0, (int)h));
+      uint32_t hdr = 0;
+      if (hend == 20u) {
+        hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
+              abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
+      } else if (hend > 20u) {  // IP options (rare): up to 60 header bytes, 5 chunks
+        for (uint32_t k = 0; k < 5; ++k) {
+          const u32x4 x = k < 3 ? hv[k] : ld16(r, (off & ~15u) + 16u * k);
+          hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
+        }
+      }
+      if (lend < flen) {  // bytes past ip_len (Ethernet padding, malformed): rare
+        for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
+          total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
+      }
+      verify_emit(verify_result(i, odd, ih, hdr_ok, l4_ok, hdr, total - hdr, d, r, off), ip_out, l4_out, st_out,
+                  bad, d);
+    }
+    if (pn >= d.n) break;
+    if (!nxt) cross();
+    // the next range becomes the current one; its first passes are in flight
+    p0 = pn;
+    off = offn;
+    flen = flenn;
+    rr = rn;
+    P = Pn;
+    pn += rstride;
+    nxt = false;
+  }
+  __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));  // no DMA outlives the wave (its LDS may be reassigned)
+}
+template <int U, int R>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_run_dma(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                                 uint8_t *st_out, uint32_t *bad) {
+  run_dma_body<U, R>(d, ip_out, l4_out, st_out, bad);
+}
+
 // RX verify of minimum-size frames in 64-byte slots (stride 64, the datagram
 // inside its slot, starting < 16 bytes in: the 64 B config, 46 B datagrams at
 // +14).  A wave owns 64 consecutive slots: four fully coalesced 1 KiB
@@ -1630,6 +1934,12 @@ MI_AQL_SHAPES(MI_AQL_SHAPE)
 MI_AQL_RUN(4)
 MI_AQL_RUN(8)
 MI_AQL_RUN(16)
+#define MI_AQL_RUN_DMA(U_, R_)                                                                           \
+  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_rundma_##U_##x##R_(                        \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                  \
+    run_dma_body<U_, R_>(d, ip, l4, st, bad);                                                            \
+  }
+MI_RUN_DMA_SHAPES(MI_AQL_RUN_DMA)
 extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st,
                                                                    uint32_t *bad) {
   slot64_body(d, ip, l4, st, bad);
@@ -1961,7 +2271,33 @@ struct Plan {
   PlanKind kind;
   Shape shape;  // kPlanShape
   int run_u;    // kPlanRun: chunks per lane per pass
+  int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
 };
+
+// The LDS-DMA flat run (k_ipv4_verify_run_dma) for packed batches with offset
+// arrays, when chosen (mi_cksum_set_run_kernel, MI_CKSUM_RUN_DMA=UxR).  Off by
+// default: on the 2^22-datagram Pareto batch it runs at the register kernel's
+// speed (198-203 vs 198 us per launch, profiles/r03/pareto_dma_r03.jsonl).
+int run_dma_shape_code(int u, int r) {
+#define X(U_, R_) if (u == U_ && r == R_) return 10 * U_ + R_;
+  MI_RUN_DMA_SHAPES(X)
+#undef X
+  return -1;
+}
+std::atomic<int> g_run_dma{-2};  // -2: not read from the environment yet
+int run_dma_code() {
+  int c = g_run_dma.load(std::memory_order_relaxed);
+  if (c == -2) {
+    const char *e = getenv("MI_CKSUM_RUN_DMA");
+    int u = 0, r = 0;
+    c = e && sscanf(e, "%dx%d", &u, &r) == 2 ? run_dma_shape_code(u, r) : 0;
+    if (c < 0) c = 0;
+    int expect = -2;
+    g_run_dma.compare_exchange_strong(expect, c);
+    c = g_run_dma.load(std::memory_order_relaxed);
+  }
+  return c;
+}
 
 Plan verify_plan(const Desc &d, uint32_t max_len) {
   // chunks per lane per pass of the flat-run kernel: 8 for packed mixed
@@ -1981,8 +2317,11 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
   if (dense_slots && d.stride == 64u && (d.first_off & 63u) < 16u && (d.first_off & 63u) + d.fixed_len <= 64u &&
       !g_tune.g && !pu_env)
     return {kPlanSlot64, {0, 0}, 0};
-  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g)
-    return {kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
+  if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
+    Plan pl{kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
+    if ((d.flags & MI_BATCH_PACKED) && d.offs && !pu_env && run_dma_code() > 0) pl.dma = run_dma_code();
+    return pl;
+  }
   if (!d.lens || g_tune.g || max_len < kClassEdges[1]) return {kPlanShape, pick_shape(max_len), 0};
   return {kPlanClasses, {0, 0}, 0};
 }
@@ -1995,6 +2334,20 @@ unsigned run_blocks(const Desc &d) {
     return v > 0 ? v : 16384;
   }();
   const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap;
+  uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+  if (blocks > (uint64_t)cap) blocks = cap;
+  return blocks ? (unsigned)blocks : 1u;
+}
+// The LDS-DMA flat run: waves loop over their ranges (the ring carries the
+// stream across them), so the grid is capped near residency;
+// MI_CKSUM_RUN_DMA_BLOCKS overrides.
+unsigned run_dma_blocks(const Desc &d) {
+  static const int env_cap = [] {
+    const char *e = getenv("MI_CKSUM_RUN_DMA_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : env_cap;
   uint64_t blocks = ((uint64_t)d.n + 255) / 256;
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
@@ -2013,6 +2366,15 @@ unsigned slot64_blocks(const Desc &d) {
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
   const Plan pl = verify_plan(d, max_len);
+  if (pl.kind == kPlanRun && pl.dma) {
+#define X(U_, R_)                                                                                            \
+  if (pl.dma == 10 * U_ + R_) {                                                                              \
+    VLAUNCH((k_ipv4_verify_run_dma<U_, R_>), dim3(run_dma_blocks(d)), dim3(kBlock), 0, s, d, ip, l4, st, bad); \
+    return launched();                                                                                       \
+  }
+    MI_RUN_DMA_SHAPES(X)
+#undef X
+  }
   if (pl.kind == kPlanRun) {
     const dim3 grid(run_blocks(d));
     if (pl.run_u == 4)
@@ -2162,19 +2524,30 @@ enum AqlKernelId {
 #define X(G_, U_) kAqlV_##G_##x##U_,
   MI_AQL_SHAPES(X)
 #undef X
-  kAqlRun4, kAqlRun8, kAqlRun16, kAqlSlot64, kAqlScalar, kAqlKernels
+  kAqlRun4, kAqlRun8, kAqlRun16,
+#define X(U_, R_) kAqlRunDma_##U_##x##R_,
+  MI_RUN_DMA_SHAPES(X)
+#undef X
+  kAqlSlot64, kAqlScalar, kAqlKernels
 };
 const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
     MI_AQL_SHAPES(X)
 #undef X
-    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_slot64", "mi_aql_scalar"};
+    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16",
+#define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
+    MI_RUN_DMA_SHAPES(X)
+#undef X
+    "mi_aql_slot64", "mi_aql_scalar"};
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
 #undef X
-    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_slot64,
-    (const void *)mi_aql_scalar};
+    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16,
+#define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
+    MI_RUN_DMA_SHAPES(X)
+#undef X
+    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar};
 
 // The kernels' explicit arguments, laid out as the compiler lays out the
 // kernel-argument segment (each parameter at its natural alignment).  The
@@ -2361,6 +2734,16 @@ int aql_kernel_for_shape(const Desc &d, Shape sh, int *id, unsigned *blocks) {
 // plan; length-class plans need several launches per pass: not offered).
 int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
   const Plan pl = verify_plan(d, max_len);
+  if (pl.kind == kPlanRun && pl.dma) {
+#define X(U_, R_)                          \
+  if (pl.dma == 10 * U_ + R_) {            \
+    *id = kAqlRunDma_##U_##x##R_;          \
+    *blocks = run_dma_blocks(d);           \
+    return 0;                              \
+  }
+    MI_RUN_DMA_SHAPES(X)
+#undef X
+  }
   if (pl.kind == kPlanRun) {
     *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
     *blocks = run_blocks(d);
@@ -2798,6 +3181,13 @@ int mi_cksum_init(int device) {
   return ensure_ctx();
 }
 
+int mi_cksum_set_run_kernel(int chunks, int slots) {
+  const int c = chunks ? run_dma_shape_code(chunks, slots) : 0;
+  if (c < 0) return set_err(-EINVAL, "no LDS-DMA flat-run kernel for %dx%d", chunks, slots);
+  g_run_dma.store(c);
+  return 0;
+}
+
 int mi_cksum_set_shape(int group, int chunks, int max_blocks) {
   if (group || chunks) {
     if (!shape_ok(group, chunks)) return set_err(-EINVAL, "no kernel for shape %dx%d", group, chunks);
@@ -2958,7 +3348,9 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
   Desc d;
   if (!b || make_desc(b, &d)) return "invalid batch";
   const Plan pl = verify_plan(d, batch_max_len(b));
-  if (pl.kind == kPlanRun)
+  if (pl.kind == kPlanRun && pl.dma)
+    snprintf(buf, sizeof buf, "k_ipv4_verify_run_dma<%d,%d>", pl.dma / 10, pl.dma % 10);
+  else if (pl.kind == kPlanRun)
     snprintf(buf, sizeof buf, "k_ipv4_verify_packed<%d>", pl.run_u);
   else if (pl.kind == kPlanShape)
     snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);

@@ -81,7 +81,8 @@ def test_no_cpu_fallback_dropin_aborts():
 
 def test_verify_plan_needs_no_gpu():
     """The kernel choice is host logic: dense minimum-size slots and hinted
-    packed layouts take the flat-run kernel, roomy slots the lane-group one."""
+    packed layouts take the flat-run kernel (packed ones its LDS-DMA form when
+    mi_cksum_set_run_kernel picks it), roomy slots the lane-group one."""
     import torch
     import libunsod_amd as mi
     buf = torch.zeros(1 << 20, dtype=torch.uint8)
@@ -91,6 +92,13 @@ def test_verify_plan_needs_no_gpu():
     offs = torch.arange(100, dtype=torch.int64) * 300
     lens = torch.full((100,), 280, dtype=torch.int32)
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8>"
+    mi.set_run_kernel(2, 4)
+    try:
+        assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_run_dma<2,4>"
+        with pytest.raises(Exception):
+            mi.set_run_kernel(3, 3)
+    finally:
+        mi.set_run_kernel(0, 0)
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens)) == "k_ipv4_verify x length classes"
     assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens // 4)) == "k_ipv4_verify<1,8>"
 

@@ -50,7 +50,7 @@ def test_demux_verify_golden(demux_golden, kernel):
     g = demux_golden
     ip, l4, st, bad, plan = _run_verify(kernel, dev(g["ver_in"]), g["offs"], g["flen"])
     if kernel == "packed":
-        assert "packed" in plan
+        assert "packed" in plan or "run_dma" in plan  # a flat-run kernel
     assert np.array_equal(ip, g["ip"]), plan
     assert np.array_equal(l4, g["l4"]), plan
     assert np.array_equal(st, g["st"]), plan

@@ -27,7 +27,53 @@ import torch  # noqa: E402
 import libunsod_amd as mi  # noqa: E402
 
 CFG = {"1500": (65536, 1500, 2176, 142), "9000": (65536, 9000, 9216, 142)}
-ROT = {"1500": (8, 24), "9000": (2, 8)}
+ROT = {"1500": (8, 24), "9000": (2, 8), "pareto": (3,)}
+
+
+def pareto(a, lib, dev, K):
+    """The Pareto batch (2^22 packed datagrams, u32 offsets, 3 rotating
+    batches as the bench): the flat-run verify kernel against a read-only flat
+    sweep of each batch's whole packed byte region, same submission."""
+    import numpy as np
+    from libunsod_amd import synth
+    n = 1 << 22
+    lens = synth.pareto_lengths(n)
+    offs = synth.packed_offsets(lens, first_off=2)
+    size = (int(offs[-1] + lens[-1]) + 256 + 255) & ~255
+    alg = int(lens.sum()) + 5 * n
+    bs, outs = [], []
+    for r in range(ROT["pareto"][0]):
+        buf = torch.empty(size, dtype=torch.uint8, device=dev)
+        b = mi.PktBatch(buf, n, offs=torch.from_numpy(offs.astype(np.int64)).to(dev),
+                        lens=torch.from_numpy(lens.astype(np.int32)).to(dev), max_len=int(lens.max()), packed=True,
+                        offs32=True)
+        mi.synth_ipv4(b, seed=0x9A7E70 + r)
+        mi.ipv4_finalize(b)
+        bs.append(b)
+        outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
+                         l4=torch.empty(n, dtype=torch.uint16, device=dev),
+                         status=torch.empty(n, dtype=torch.uint8, device=dev)))
+    torch.cuda.synchronize()
+    rep = mi.VerifyRepeat(bs, outs, nstreams=2)
+    rep.run(100)
+    bases = (C.c_void_p * len(bs))(*[b.buf.data_ptr() for b in bs])
+    flat = size & ~15
+    for rnd in range(a.rounds):
+        rep.run(K, timed=True)
+        span = rep.span()
+        us = span / K
+        print(json.dumps(dict(config="pareto", round=rnd, kernel=mi.verify_plan(bs[0]), us_per_launch=round(us, 3),
+                              alg_TBps=round(alg / us / 1e6, 3), frac_8TBps=round(alg / us / 8e6, 4))), flush=True)
+        for unroll in (4, 8, 16):
+            for grid in (2048, 8192, 32768):
+                sp = lib.ceil_run(bases, len(bs), size, 1, 0, 0, flat // 16, 1, unroll, grid, K, 2)
+                if sp <= 0:
+                    raise SystemExit(f"ceil_run failed: {sp}")
+                u = sp / K
+                print(json.dumps(dict(config="pareto", round=rnd, kernel="probe_flat", unroll=unroll, grid=grid,
+                                      us_per_launch=round(u, 3), read_TBps=round(flat / u / 1e6, 3),
+                                      alg_TBps_at_probe=round(alg / u / 1e6, 3))), flush=True)
+    rep.close()
 
 
 def main():
@@ -44,6 +90,9 @@ def main():
     torch.cuda.set_device(0)
     K = a.steps
     for cfg in a.configs.split(","):
+        if cfg == "pareto":
+            pareto(a, lib, dev, K)
+            continue
         n, L, stride, first = CFG[cfg]
         size = (first + (n - 1) * stride + L + 64 + 255) & ~255
         env_off = first & ~15
@@ -67,7 +116,8 @@ def main():
             bases = (C.c_void_p * R)(*[b.buf.data_ptr() for b in bs])
             between = (R - 1) * env_bytes
             for rnd in range(a.rounds):
-                span = rep.run(K, timed=True)
+                rep.run(K, timed=True)
+                span = rep.span()
                 us = span / K
                 print(json.dumps(dict(config=cfg, R=R, read_between_reuse_MB=round(between / 1e6), round=rnd,
                                       kernel=mi.verify_plan(bs[0]), us_per_launch=round(us, 3),
