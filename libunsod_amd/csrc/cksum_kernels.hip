@@ -83,8 +83,16 @@ __device__ __forceinline__ void verify_body(const Desc &d, uint16_t *ip_out, uin
   });
   if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
+// (Holding the U <= 6 shapes to 6 waves per SIMD -- 16x6 at 80 VGPRs instead
+// of 91 -- was built and measured: the 2-queue headline unchanged, 14.16-14.31
+// vs 14.16-14.31 us per pass over 400 steps; one stream 18.4-18.7 vs 18.4-20.0;
+// profiles/r03/verify_waves_r03.jsonl.  Default bound kept.)
+template <int U>
+constexpr int verify_waves_per_simd() {
+  return 1;
+}
 template <int G, int U>
-__global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+__global__ __launch_bounds__(kBlock, verify_waves_per_simd<U>()) void k_ipv4_verify(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                                         uint32_t *bad) {
   verify_body<G, U>(d, ip_out, l4_out, st_out, bad);
 }
@@ -96,8 +104,20 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify(Desc d, uint16_t *ip_out
 // batch -- and with it the buffer resource -- is uniform per wave (scalar
 // loads of the kernel-argument table, no waterfall).
 
+// A resident grid loops over its units, so the kernel is as fast as its
+// occupancy: shapes with U == 2 are held to 6 waves per SIMD (80 VGPRs; 8x2
+// takes 81 -- 5 waves -- otherwise), U <= 6 to 5 (96 VGPRs; 16x6 would take
+// 117 and run at 4).  (Wider shapes would spill.)  Measured on one stream,
+// 16 x 1500 B batches per launch (profiles/r03/multi_r03.jsonl): 16x6 18.7 ->
+// 17.1 us per batch, 8x4 16.1 -> 15.7, 8x2 16.1 -> 15.9.  Dealing the units to
+// the waves in 2 or 4 interleaved streams (the running waves reading 2-4
+// distant regions instead of one window) measured 0.5-1.5 us per batch slower.
+template <int U>
+constexpr int multi_waves_per_simd() {
+  return U == 2 ? 6 : U <= 6 ? 5 : 1;
+}
 template <int G, int U>
-__global__ __launch_bounds__(kBlock) void k_ipv4_verify_multi(MultiArgs a) {
+__global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_verify_multi(MultiArgs a) {
   constexpr uint32_t gpw = 64u / G;
   const int lane = threadIdx.x & (G - 1);
   const uint32_t gid = (threadIdx.x & 63u) / G;
@@ -1920,7 +1940,7 @@ constexpr int kScalarThreads = 512;
 // kernel descriptors by name in the code object HIP loaded and dispatch them
 // with packets it writes itself.  One argument list for all of them.
 #define MI_AQL_SHAPE(G_, U_)                                                                            \
-  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_v_##G_##x##U_(                           \
+  extern "C" __global__ __launch_bounds__(kBlock, verify_waves_per_simd<U_>()) void mi_aql_v_##G_##x##U_(                           \
       Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
     verify_body<G_, U_>(d, ip, l4, st, bad);                                                            \
   }
