@@ -1123,6 +1123,9 @@ __device__ __forceinline__ uint32_t group_fold(__amdgpu_buffer_rsrc_t r, uint32_
   return fold16(group_sum<G>(acc));
 }
 
+#ifndef MI_CHAIN_LOAD_AUX
+#define MI_CHAIN_LOAD_AUX 2
+#endif
 // Fast path of k_chain: a chain whose selected bytes fall in at most
 // kChainPieces nonempty mbufs (the socket-buffer and rte_mbuf chains: a header
 // mbuf and 1-2 cluster pieces).  The group loads the chain's (m_data, m_len)
@@ -1208,7 +1211,8 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
             const uint32_t A = j3 ? A3 : j2 ? A2 : j1 ? A1 : A0;
             const uint32_t P = j3 ? P3 : j2 ? P2 : j1 ? P1 : 0u;
             pc[u] = c;
-            v[u] = ld16(r, c < T ? (A & ~15u) + 16u * (c - P) : kOOB);
+            v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, c < T ? (A & ~15u) + 16u * (c - P) : kOOB, 0,
+                                                         MI_CHAIN_LOAD_AUX);
           }
 #pragma unroll
           for (int u = 0; u < U; ++u) {
@@ -1518,6 +1522,22 @@ __device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, cons
 // load that would start before the source buffer or run past its end takes a
 // per-byte path instead (the first / last bytes of the buffer only).
 constexpr int kTxSeg = 4;
+// The source loads of the TX gather.  A group's 16-byte loads start at any
+// byte, so each wave-instruction's window of a frame straddles one more
+// 128-byte line than it covers, and the next pass's window starts in that same
+// line: with nontemporal loads (which do not keep the line in L2) every such
+// line came from HBM twice -- 1.45x the algorithmic read bytes, from the
+// request-size counters (32 B x RDREQ_32B + 64 B x RDREQ_64B + 128 B x
+// RDREQ_128B; profiles/r03/pmc_reqsize_r03.jsonl).  With the default policy
+// (MI_TX_LOAD_AUX 0) the straddled line is an L2 hit: 1.15x, and socket frames
+// 51.5 -> 47.1 us per 65536 x 1514 B batch (0.48 -> 0.53 of 8 TB/s),
+// single-segment frames 48.1 -> 44.4 us (0.51 -> 0.56); profiles/r03/tx_r03.jsonl.
+#ifndef MI_TX_LOAD_AUX
+#define MI_TX_LOAD_AUX 0
+#endif
+__device__ __forceinline__ u32x4 ld16_src(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MI_TX_LOAD_AUX);
+}
 // MI_TX_PIPE=1: the frame's passes software-pipelined (below).  Measured on
 // MI355X (profiles/tx_pipe_r02.jsonl, same box, interleaved): socket frames
 // 57.9 us per launch against 51.3 one pass at a time, single-segment frames
@@ -1848,8 +1868,8 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         for (int u = 0; u < U; ++u) {
           const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
           const bool in = p < npass && !c.slow;
-          a[u] = ld16(rs, in && c.q0 < sg.L ? c.A1 : kOOB);
-          b[u] = ld16(rs, in && c.two ? c.A2 : kOOB);
+          a[u] = ld16_src(rs, in && c.q0 < sg.L ? c.A1 : kOOB);
+          b[u] = ld16_src(rs, in && c.two ? c.A2 : kOOB);
         }
       };
       issue(0, xa, xb);
@@ -1873,8 +1893,8 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
-          xa[u] = ld16(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
-          xb[u] = ld16(rs, c.two && !c.slow ? c.A2 : kOOB);
+          xa[u] = ld16_src(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
+          xb[u] = ld16_src(rs, c.two && !c.slow ? c.A2 : kOOB);
           cut[u] = c;
         }
         if (p == 0) prefetch2();
@@ -2201,7 +2221,12 @@ Shape pick_shape(uint32_t max_len) {
 }
 
 int grid_for(uint32_t n, int G) {
-  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 2048;
+  static const int env_cap = [] {  // MI_CKSUM_GRID_CAP: the default cap (tuning experiments)
+    const char *e = getenv("MI_CKSUM_GRID_CAP");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 2048;
+  }();
+  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : env_cap;
   const uint64_t groups_per_block = kBlock / G;
   uint64_t blocks = (n + groups_per_block - 1) / groups_per_block;
   if (blocks > (uint64_t)cap) blocks = cap;
