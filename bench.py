@@ -257,16 +257,19 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
     achieved = alg_bytes / gpu_s_per_launch / 1e9
     config = wl.get("name", args.config)
     traffic, tsrc = None, None
-    tfile = os.path.join(ROOT, "profiles", "pmc_traffic_r02.json")
+    # HBM bytes per launch from the newest PMC record of this config (request-
+    # size counters, round 3; FETCH_SIZE x2, round 2), labelled with its source
     tkey = config + ("_u64" if args.offs64 else "_u32") if config == "pareto" else config
-    if os.path.exists(tfile):
+    for rel in ("profiles/r03/pmc_traffic_r03.json", "profiles/pmc_traffic_r02.json"):
+        tfile = os.path.join(ROOT, rel)
         try:
-            ent = json.load(open(tfile)).get(tkey)
-            if ent:
-                traffic = ent["bytes_per_launch"]
-                tsrc = f"profiles/pmc_traffic_r02.json[{tkey}] (rocprofv3 --pmc, separate passes; not this run)"
+            ent = json.load(open(tfile)).get(tkey) if os.path.exists(tfile) else None
         except Exception:
-            traffic = None
+            ent = None
+        if ent:
+            traffic = ent["bytes_per_launch"]
+            tsrc = f"{rel}[{tkey}] (rocprofv3 --pmc, separate passes; not this run)"
+            break
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
                 kernel=mi.verify_plan(batches[0]) + (" (its AQL entry point mi_aql_*)" if rep is not None and
