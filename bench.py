@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--also", default="auto",
                     help="a second config timed in the same run and reported as config_<name> (auto: 9000 when "
                          "the config is 1500 -- the metric names both frame sizes; none: off)")
+    ap.add_argument("--outputs", default="all", choices=["all", "status"],
+                    help="status: store only the per-datagram status byte (an RX drop decision); the default "
+                         "stores ip / l4 sums and status (5 B per datagram)")
     ap.add_argument("--sustain-seconds", type=float, default=3.0,
                     help="after the timed region, re-run the same passes back to back this long (reported as "
                          "'sustained', not part of value; 0 = off)")
@@ -89,7 +92,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev, rank: int, world: int):
+def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev, rank: int, world: int,
+                   outputs: str = "all"):
     """The batches of one config on this rank: R rotating device batches,
     device-generated and TX-finalized so every packet verifies."""
     if config == "pareto":
@@ -136,16 +140,22 @@ def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev
         mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r + 104729 * rank)
         mi.ipv4_finalize(b)  # TX path makes every packet valid
         batches.append(b)
-        outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
-                         l4=torch.empty(n, dtype=torch.uint16, device=dev),
-                         status=torch.empty(n, dtype=torch.uint8, device=dev)))
+        if outputs == "status":  # the RX drop decision alone (ip / l4 sums not stored)
+            outs.append(dict(status=torch.empty(n, dtype=torch.uint8, device=dev)))
+        else:
+            outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
+                             l4=torch.empty(n, dtype=torch.uint16, device=dev),
+                             status=torch.empty(n, dtype=torch.uint8, device=dev)))
     torch.cuda.synchronize()
     chk = mi.ipv4_verify(batches[0], bad_count=True)  # sanity: everything verifies
     torch.cuda.synchronize()
     if int(chk["bad"].item()) != 0:
         raise SystemExit(f"rank {rank}: synthetic batch does not verify ({int(chk['bad'].item())} bad)")
     lay = (dict(stride=stride, first_off=first, fixed_len=L) if lens is None else dict(offs=offs, lens=lens))
-    return dict(batches=batches, outs=outs, n=n, L_sum=L_sum, cfg=cfg, scaling=scaling, lay=lay)
+    if outputs == "status":
+        cfg["outputs"] = "status byte only (the RX drop decision; ip / l4 sums not stored)"
+    return dict(batches=batches, outs=outs, n=n, L_sum=L_sum, cfg=cfg, scaling=scaling, lay=lay,
+                out_bytes=1 if outputs == "status" else 5)
 
 
 def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_s: float = 0.0) -> dict:
@@ -253,7 +263,7 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
     # overlap, so this is the GPU time each launch costs; rocprof's union of
     # dispatch intervals / K is the same quantity (tools/prof_summary.py).
     gpu_s_per_launch = span_us / K / 1e6
-    alg_bytes = float(L_sum) + 5.0 * n
+    alg_bytes = float(L_sum) + float(wl.get("out_bytes", 5)) * n
     achieved = alg_bytes / gpu_s_per_launch / 1e9
     config = wl.get("name", args.config)
     traffic, tsrc = None, None
@@ -335,7 +345,7 @@ def main():
     if args.wait == "busy":
         mi.set_busy_wait(True)
 
-    wl = build_workload(mi, synth, shard, args.config, args.rotate, args.offs64, dev, rank, world)
+    wl = build_workload(mi, synth, shard, args.config, args.rotate, args.offs64, dev, rank, world, args.outputs)
     wl["name"] = args.config
     K = args.steps
     m = measure(mi, shard, wl, args, K, dev, dist, backend, sustain_s=args.sustain_seconds)
