@@ -1126,6 +1126,9 @@ __device__ __forceinline__ uint32_t group_fold(__amdgpu_buffer_rsrc_t r, uint32_
 #ifndef MI_CHAIN_LOAD_AUX
 #define MI_CHAIN_LOAD_AUX 2
 #endif
+#ifndef MI_CHAIN_PREFETCH
+#define MI_CHAIN_PREFETCH 1
+#endif
 // Fast path of k_chain: a chain whose selected bytes fall in at most
 // kChainPieces nonempty mbufs (the socket-buffer and rte_mbuf chains: a header
 // mbuf and 1-2 cluster pieces).  The group loads the chain's (m_data, m_len)
@@ -1149,17 +1152,77 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
   const int lane = threadIdx.x & (G - 1);
   const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
-  for (uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G; i < cd.n; i += stride) {
-    uint32_t k = cd.pkt_seg[i];
-    const uint32_t kend = cd.pkt_seg[i + 1];
-    uint64_t sum = 0;
-    // ---- fast path: one mbuf per lane, pieces by a group scan
-    const int64_t lo = cd.skip[i];
-    const int64_t hi = cd.pseudo ? lo + (int64_t)cd.len[i] : (int64_t)cd.len[i];
-    const uint32_t nseg = kend > k ? kend - k : 0u;
+  // MI_CHAIN_PREFETCH: the next chain's descriptors (pkt_seg pair, skip, len:
+  // at the top of a chain; its first G segments: once this chain's first data
+  // loads are out) land while this chain's data is in flight, instead of two
+  // dependent round trips ahead of every chain's first load.  Socket chains
+  // 18.7-18.9 -> 18.2-18.5 us per 65536 (profiles/r03/chain_r03.jsonl); the
+  // grid cap (1024-8192) and the source-load policy measured flat.
+  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
+  uint32_t k_c = 0, kend_c = 0, ln_c = 0;
+  int64_t lo_c = 0;
+  int32_t ml_c = 0;
+  uint64_t so_c = 0;
+  auto level1 = [&](uint32_t j, uint32_t &kk, uint32_t &ke, int64_t &sk, uint32_t &ln) {
+    kk = ke = ln = 0;
+    sk = 0;
+    if (j < cd.n) {
+      kk = cd.pkt_seg[j];
+      ke = cd.pkt_seg[j + 1];
+      sk = cd.skip[j];
+      ln = (uint32_t)cd.len[j];
+    }
+  };
+  auto level2 = [&](uint32_t kk, uint32_t ke, int32_t &m, uint64_t &o) {
+    const uint32_t ns = ke > kk ? ke - kk : 0u;
+    m = 0;
+    o = 0;
+    if ((uint32_t)lane < ns && ns <= (uint32_t)G) {
+      m = cd.seg_len[kk + lane];
+      o = cd.seg_off[kk + lane];
+    }
+  };
+  if (MI_CHAIN_PREFETCH) {
+    level1(i, k_c, kend_c, lo_c, ln_c);
+    level2(k_c, kend_c, ml_c, so_c);
+  }
+  for (; i < cd.n; i += stride) {
+    uint32_t k, kend, ln_i;
+    int64_t lo;
     int32_t ml = 0;
     uint64_t so = 0;
-    if ((uint32_t)lane < nseg && nseg <= (uint32_t)G) {
+    const uint32_t in = i + stride;
+    uint32_t k_n = 0, kend_n = 0, ln_n = 0;
+    int64_t lo_n = 0;
+    bool pre2 = false;
+    if (MI_CHAIN_PREFETCH) {
+      k = k_c;
+      kend = kend_c;
+      lo = lo_c;
+      ln_i = ln_c;
+      ml = ml_c;
+      so = so_c;
+      level1(in, k_n, kend_n, lo_n, ln_n);
+    } else {
+      k = cd.pkt_seg[i];
+      kend = cd.pkt_seg[i + 1];
+      lo = cd.skip[i];
+      ln_i = (uint32_t)cd.len[i];
+    }
+    auto prefetch2 = [&]() {
+      if (!MI_CHAIN_PREFETCH || pre2) return;
+      pre2 = true;
+      level2(k_n, kend_n, ml_c, so_c);
+      k_c = k_n;
+      kend_c = kend_n;
+      lo_c = lo_n;
+      ln_c = ln_n;
+    };
+    uint64_t sum = 0;
+    // ---- fast path: one mbuf per lane, pieces by a group scan
+    const int64_t hi = cd.pseudo ? lo + (int64_t)(int32_t)ln_i : (int64_t)(int32_t)ln_i;
+    const uint32_t nseg = kend > k ? kend - k : 0u;
+    if (!MI_CHAIN_PREFETCH && (uint32_t)lane < nseg && nseg <= (uint32_t)G) {
       ml = cd.seg_len[k + lane];
       so = cd.seg_off[k + lane];
     }
@@ -1214,6 +1277,7 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
             v[u] = __builtin_amdgcn_raw_buffer_load_b128(r, c < T ? (A & ~15u) + 16u * (c - P) : kOOB, 0,
                                                          MI_CHAIN_LOAD_AUX);
           }
+          if (p == 0) prefetch2();
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const uint32_t c = pc[u];
@@ -1232,9 +1296,11 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
         }
         sum += fold16(group_sum<G>(acc));
         if (lane == 0) out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+        prefetch2();
         continue;
       }
     }
+    prefetch2();
     // ---- general walk (long chains, negative m_len, off0 past the first mbuf)
     int64_t clen = 0;
     // fold one piece of the chain: `mlen` bytes at buffer offset `a`
