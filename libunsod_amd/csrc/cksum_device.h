@@ -558,6 +558,15 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
 #define MI_DEFER 0
 #endif
 constexpr bool kDefer = MI_DEFER;
+// MI_OUT_AUX >= 0: the ip / l4 / status stores as buffer stores with that
+// cache policy (gfx950 CPol bits: 1 = sc0, 2 = nt, 16 = sc1); -1 (default):
+// plain global stores.  Measured (profiles/r03/serial_floor_r03.jsonl), 1500 B
+// verify per launch on one stream / two queues: default 18.5 / 14.24, sc0
+// 18.3-18.7, sc1 19.3-19.6 / 15.0, sc0+sc1 19.2-19.6 / 15.1, nt 20.2-20.7 /
+// 18.5-18.7 (partial-line nt writes) -- plain stores stay.
+#ifndef MI_OUT_AUX
+#define MI_OUT_AUX -1
+#endif
 struct VOut {
   uint32_t i = ~0u;  // ~0u: nothing pending
   uint32_t ip = 0, l4 = 0, st = 0, fl = 0, cd = 0;
@@ -597,9 +606,22 @@ __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr 
 __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const Desc &d) {
   if (o.i == ~0u) return;
+#if MI_OUT_AUX >= 0
+  constexpr int kOA = MI_OUT_AUX;
+  if (ip_out)
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o.ip, __builtin_amdgcn_make_buffer_rsrc(ip_out, 0, 0x7fffffff, 0x00020000),
+                                          2u * o.i, 0, kOA);
+  if (l4_out)
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o.l4, __builtin_amdgcn_make_buffer_rsrc(l4_out, 0, 0x7fffffff, 0x00020000),
+                                          2u * o.i, 0, kOA);
+  if (st_out)
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.st, __builtin_amdgcn_make_buffer_rsrc(st_out, 0, 0x7fffffff, 0x00020000),
+                                         o.i, 0, kOA);
+#else
   if (ip_out) ip_out[o.i] = (uint16_t)o.ip;
   if (l4_out) l4_out[o.i] = (uint16_t)o.l4;
   if (st_out) st_out[o.i] = (uint8_t)o.st;
+#endif
   if (bad && (o.st & ~MI_ST_L4_NONE)) atomicAdd(bad, 1u);
   if (d.cflags) {
     d.cflags[o.i] = o.fl;

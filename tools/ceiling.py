@@ -81,6 +81,14 @@ def main():
     ap.add_argument("--configs", default="1500,9000")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="1 = every launch serialized after the previous one on one stream (the\n"
+                         "single-submission case, VERDICT r2 item 4): the probe then shows what ANY\n"
+                         "read kernel of these bytes pays per serialized launch")
+    ap.add_argument("--grids", default="2048,4096,8192")
+    ap.add_argument("--modes", default="0,1", help="ceil_run modes (tools/ceiling_probe.hip); 4 = the\n"
+                    "envelope read plus 4 B per slot into a dense side array, i.e. verify's writes")
+    ap.add_argument("--outputs", choices=("all", "status"), default="all")
     a = ap.parse_args()
     lib = C.CDLL(os.path.join(ROOT, "tools", "libceiling.so"))
     lib.ceil_run.restype = C.c_float
@@ -107,11 +115,13 @@ def main():
                 mi.synth_ipv4(b, seed=0x5EED5EED + 7919 * r)
                 mi.ipv4_finalize(b)
                 bs.append(b)
-                outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device=dev),
-                                 l4=torch.empty(n, dtype=torch.uint16, device=dev),
-                                 status=torch.empty(n, dtype=torch.uint8, device=dev)))
+                o = dict(status=torch.empty(n, dtype=torch.uint8, device=dev))
+                if a.outputs == "all":
+                    o.update(ip=torch.empty(n, dtype=torch.uint16, device=dev),
+                             l4=torch.empty(n, dtype=torch.uint16, device=dev))
+                outs.append(o)
             torch.cuda.synchronize()
-            rep = mi.VerifyRepeat(bs, outs, nstreams=2)
+            rep = mi.VerifyRepeat(bs, outs, nstreams=a.streams)
             rep.run(2000)  # settle
             bases = (C.c_void_p * R)(*[b.buf.data_ptr() for b in bs])
             between = (R - 1) * env_bytes
@@ -119,19 +129,20 @@ def main():
                 rep.run(K, timed=True)
                 span = rep.span()
                 us = span / K
-                print(json.dumps(dict(config=cfg, R=R, read_between_reuse_MB=round(between / 1e6), round=rnd,
-                                      kernel=mi.verify_plan(bs[0]), us_per_launch=round(us, 3),
+                print(json.dumps(dict(config=cfg, R=R, streams=a.streams, read_between_reuse_MB=round(between / 1e6), round=rnd,
+                                      kernel=mi.verify_plan(bs[0]), outputs=a.outputs, us_per_launch=round(us, 3),
                                       alg_TBps=round(alg / us / 1e6, 3), frac_8TBps=round(alg / us / 8e6, 4),
                                       env_TBps=round(env_bytes / us / 1e6, 3))), flush=True)
-                for mode in (0, 1):
+                for mode in [int(m) for m in a.modes.split(",")]:
                     for unroll in (4, 8, 16):
-                        for grid in (2048, 4096, 8192):
-                            sp = lib.ceil_run(bases, R, size, n, stride, env_off, nch, mode, unroll, grid, K, 2)
+                        for grid in [int(g) for g in a.grids.split(",")]:
+                            sp = lib.ceil_run(bases, R, size, n, stride, env_off, nch, mode, unroll, grid, K,
+                                              a.streams)
                             if sp <= 0:
                                 raise SystemExit(f"ceil_run failed: {sp}")
                             u = sp / K
-                            print(json.dumps(dict(config=cfg, R=R, round=rnd,
-                                                  kernel=("probe_env" if mode == 0 else "probe_flat"),
+                            print(json.dumps(dict(config=cfg, R=R, streams=a.streams, round=rnd,
+                                                  kernel={0: "probe_env", 1: "probe_flat", 4: "probe_env_w4dense"}.get(mode, f"mode{mode}"),
                                                   unroll=unroll, grid=grid, us_per_launch=round(u, 3),
                                                   read_TBps=round(env_bytes / u / 1e6, 3))), flush=True)
             rep.close()

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void rd_env(const uint8_t *p, uint32_t bytes, 
 // ip_sum / L4 sum patch of in_delayed_cksum + ip_sum); WMODE 2: the lanes
 // holding chunks 0..3 store them back whole (one full 64 B block per slot);
 // WMODE 3: 4 bytes per slot into a separate dense array (what verify writes).
-// SAUX: the stores' cache policy (2 = nontemporal).
+// SAUX: the stores' cache policy (gfx950 CPol bits: 1 = sc0, 2 = nt, 16 = sc1).
 template <int U, int WMODE, int SAUX = 0>
 __global__ __launch_bounds__(256) void rdw_env(uint8_t *p, uint32_t bytes, uint32_t nslots, uint32_t stride,
                                               uint32_t env_off, uint32_t nch, uint32_t *side) {
@@ -79,7 +79,9 @@ __global__ __launch_bounds__(256) void rdw_env(uint8_t *p, uint32_t bytes, uint3
       acc += x;
       if (WMODE == 1 && k[u] == 0) __builtin_amdgcn_raw_buffer_store_b32(x | 1u, r, a + 8u, 0, SAUX);
       if (WMODE == 2 && k[u] < 4) __builtin_amdgcn_raw_buffer_store_b128(v[u], r, a, 0, SAUX);
-      if (WMODE == 3 && k[u] == 0) side[slot[u]] = x;
+      if (WMODE == 3 && k[u] == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(x, __builtin_amdgcn_make_buffer_rsrc(side, 0, (int)(nslots * 4u), 0x00020000),
+                                              4u * slot[u], 0, SAUX);
     }
   }
   if (acc == 0x9E3779B9u) side[0] = acc;
@@ -224,7 +226,14 @@ float ceil_run(void *const *bases, int nb, uint32_t bytes, uint32_t nslots, uint
     hipLaunchKernelGGL((rdw_env<U, 1, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
   else if (mode == 6)                                                                                \
     hipLaunchKernelGGL((rdw_env<U, 2, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
-  else                                                                                               \
+  else if (mode >= 8 && mode <= 12) {                                                                \
+    const int aux = mode == 8 ? 2 : mode == 9 ? 1 : mode == 10 ? 16 : mode == 11 ? 17 : 3;          \
+    if (aux == 2) hipLaunchKernelGGL((rdw_env<U, 3, 2>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+    else if (aux == 1) hipLaunchKernelGGL((rdw_env<U, 3, 1>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+    else if (aux == 16) hipLaunchKernelGGL((rdw_env<U, 3, 16>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+    else if (aux == 17) hipLaunchKernelGGL((rdw_env<U, 3, 17>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+    else hipLaunchKernelGGL((rdw_env<U, 3, 3>), dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off, nch, side); \
+  } else                                                                                             \
     hipLaunchKernelGGL(wr_patch, dim3(grid), dim3(256), 0, st, (uint8_t *)p, bytes, nslots, stride, env_off);
     if (unroll == 2) { L(2) } else if (unroll == 4) { L(4) } else if (unroll == 8) { L(8) } else { L(16) }
 #undef L
