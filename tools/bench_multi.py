@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--shapes", default="auto", help="lane-group shapes GxU to sweep (auto: the library's choice)")
     ap.add_argument("--caps", default="0", help="workgroup caps to sweep (0: the library default -- a resident-sized grid for "
                                                 "the multi-batch launch, 2048 for single launches)")
+    ap.add_argument("--offs", action="store_true", help="describe the slots by an int64 offset array (descriptor loads)")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     n, L, stride, first = CFG[a.config]
@@ -42,6 +43,9 @@ def main():
                         fixed_len=L)
         mi.synth_ipv4(b, seed=r + 9)
         mi.ipv4_finalize(b)
+        if a.offs:
+            b = mi.PktBatch(b.buf, n, offs=first + torch.arange(n, dtype=torch.int64, device="cuda") * stride,
+                            fixed_len=L)
         bs.append(b)
         outs.append(dict(ip=torch.empty(n, dtype=torch.uint16, device="cuda"),
                          l4=torch.empty(n, dtype=torch.uint16, device="cuda"),
@@ -74,7 +78,7 @@ def main():
             e1.record(s)
         s.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / (launches * m)
-        print(json.dumps(dict(config=a.config, shape=f"{g}x{u}" if g else "auto", batches_per_launch=m, launches=launches, streams=1, cap=cap or "default",
+        print(json.dumps(dict(config=a.config, layout="offs" if a.offs else "stride", shape=f"{g}x{u}" if g else "auto", batches_per_launch=m, launches=launches, streams=1, cap=cap or "default",
                               us_per_batch=round(us, 3), frac=round(alg / us / 8e6, 4),
                               GiBps=round(n * L / (us * 1e-6) / 2**30, 1))), flush=True)
 
