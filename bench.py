@@ -70,8 +70,9 @@ def parse():
     ap.add_argument("--settle", type=float, default=0.3,
                     help="untimed warm-up lasts at least this many seconds (GPU clock settle)")
     ap.add_argument("--also", default="auto",
-                    help="a second config timed in the same run and reported as config_<name> (auto: 9000 when "
-                         "the config is 1500 -- the metric names both frame sizes; none: off)")
+                    help="comma-separated configs timed in the same run after the main one, each reported as "
+                         "config_<name> with its own roofline (auto: 9000,64,pareto when the config is 1500 -- the "
+                         "metric names 1500 B and 9000 B frames, BASELINE.json lists the other two; none: off)")
     ap.add_argument("--outputs", default="all", choices=["all", "status"],
                     help="status: store only the per-datagram status byte (an RX drop decision); the default "
                          "stores ip / l4 sums and status (5 B per datagram)")
@@ -80,11 +81,15 @@ def parse():
                          "'sustained', not part of value; 0 = off)")
     a = ap.parse_args()
     if a.also == "auto":
-        a.also = "9000" if a.config == "1500" else ""
+        a.also = ["9000", "64", "pareto"] if a.config == "1500" else []
     elif a.also == "none":
-        a.also = ""
-    elif a.also not in list(CONFIGS) + ["pareto"]:
-        ap.error(f"--also {a.also}: unknown config")
+        a.also = []
+    else:
+        a.also = [c for c in a.also.split(",") if c]
+        for c in a.also:
+            if c not in list(CONFIGS) + ["pareto"]:
+                ap.error(f"--also {c}: unknown config")
+    a.also = [c for c in a.also if c != a.config]
     return a
 
 
@@ -158,6 +163,40 @@ def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev
                 out_bytes=1 if outputs == "status" else 5)
 
 
+POISON = {"ip": -1, "l4": -1, "status": 0xFF}  # no verdict of a verify pass: status bits are 1/2/4/8
+
+
+def poison_outputs(outs) -> None:
+    for o in outs:
+        for k, t in o.items():
+            t.fill_(POISON[k])
+    torch.cuda.synchronize()
+
+
+def check_timed_outputs(outs, K: int) -> dict:
+    """After the timed region: the K passes went to K distinct rotating batches
+    (or all R of them when K >= R); each such batch's outputs must be the
+    verdicts of valid datagrams (ip = l4 = status = 0 everywhere: the batches
+    are TX-finalized), every other batch must still hold the poison.  Raises if
+    not -- a line whose timed passes did not verify every datagram is never
+    printed."""
+    written = untouched = 0
+    for o in outs:
+        st = o["status"]
+        if bool((st == 0).all()) and all(bool((o[k] == 0).all()) for k in ("ip", "l4") if k in o):
+            written += 1
+        elif bool((st == 0xFF).all()):
+            untouched += 1
+        else:
+            raise SystemExit("timed outputs: a batch is partly written or holds a failed verdict")
+    if written != min(K, len(outs)) or written + untouched != len(outs):
+        raise SystemExit(f"timed outputs: {written} batches written by {K} passes over {len(outs)}")
+    return dict(checked=True, batches_written=written, batches_rotating=len(outs),
+                datagrams_checked=written * int(outs[0]["status"].numel()),
+                rule="outputs poisoned before the region; after it every batch the K passes covered holds "
+                     "ip = l4 = status = 0 for every datagram (read back untimed), the rest the poison")
+
+
 def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_s: float = 0.0) -> dict:
     """Warm up, then time exactly K verify passes over the rotating batches,
     bracketed by a barrier + torch.cuda.synchronize() on both sides, max over
@@ -228,6 +267,12 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
         w = round((time.perf_counter() - ta) * 1e6, 1)
         warm_walls.append((w, round(rep.span(), 1)) if rep is not None else w)
 
+    # Poison every rotating batch's outputs (untimed): after the region, the
+    # batches its K passes covered must hold the verdicts of valid datagrams
+    # (all zero) and the others the poison -- proof that the timed passes did
+    # the work (check_timed_outputs).
+    poison_outputs(outs)
+
     # ------------------------------------------------------- timed region
     if dist:
         dist.barrier()
@@ -251,6 +296,7 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
             trace["t1"] = round((t1 - t0) * 1e6, 1)
     if dist:
         dist.barrier()
+    checked = check_timed_outputs(outs, K)
     my_bytes = float(L_sum) * K
     elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, my_bytes, float(n) * K,
                                                     device=dev if dist and backend == "nccl" else None)
@@ -294,7 +340,7 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
     roof["isolated_achieved"] = round(alg_bytes / (float(np.median(iso_us)) / 1e6) / 1e9, 1)
     out = dict(value=round(value, 2), ms_per_step=round(elapsed / K * 1e3, 5), config=cfg,
                mpkt_per_s=round(job_pkts / elapsed / 1e6, 2), roofline=roof, my_bytes=my_bytes,
-               my_elapsed=t1 - t0, job_pkts=job_pkts, elapsed=elapsed)
+               my_elapsed=t1 - t0, job_pkts=job_pkts, elapsed=elapsed, timed_outputs=checked)
     if warm_walls:
         out["warm_region_walls_us"] = warm_walls
     if trace:
@@ -356,20 +402,25 @@ def main():
         "data": "synthetic: device-generated IPv4/TCP datagrams (splitmix64 payload), TX-finalized to valid sums",
         "config": m["config"], "mpkt_per_s": m["mpkt_per_s"], "roofline": m["roofline"],
     }
-    for k in ("warm_region_walls_us", "host_trace_us", "sustained"):
+    result["timed_outputs_checked"] = m["timed_outputs"]["checked"]
+    for k in ("warm_region_walls_us", "host_trace_us", "sustained", "timed_outputs"):
         if k in m:
             result[k] = m[k]
-    if args.config == "64":
-        # every 46 B datagram is one 64 B minimum Ethernet frame (14 B header +
-        # 46 B + 4 B FCS): the frame-equivalent rate SURVEY.md 8(d) asks for
-        result["frame64_equiv_gibs"] = round(m["job_pkts"] * 64 / m["elapsed"] / GIB, 2)
-    if dist:
-        # per-GPU rates (SURVEY.md 8(e) "Reporting"): timing bookkeeping only
-        mine = torch.tensor([m["my_bytes"], m["my_elapsed"]], dtype=torch.float64,
-                            device=dev if backend == "nccl" else None)
-        allr = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(allr, mine)
-        result["per_gpu"] = [round(float(x[0]) / float(x[1]) / GIB, 2) for x in allr]
+
+    def per_config_extras(dst: dict, cfg_name: str, mm: dict) -> None:
+        if cfg_name == "64":
+            # every 46 B datagram is one 64 B minimum Ethernet frame (14 B header +
+            # 46 B + 4 B FCS): the frame-equivalent rate SURVEY.md 8(d) asks for
+            dst["frame64_equiv_gibs"] = round(mm["job_pkts"] * 64 / mm["elapsed"] / GIB, 2)
+        if dist:
+            # per-GPU rates (SURVEY.md 8(e) "Reporting"): timing bookkeeping only
+            mine = torch.tensor([mm["my_bytes"], mm["my_elapsed"]], dtype=torch.float64,
+                                device=dev if backend == "nccl" else None)
+            allr = [torch.zeros_like(mine) for _ in range(world)]
+            dist.all_gather(allr, mine)
+            dst["per_gpu"] = [round(float(x[0]) / float(x[1]) / GIB, 2) for x in allr]
+
+    per_config_extras(result, args.config, m)
 
     # -------------------------------------------- CPU baseline + host path
     host = None
@@ -380,17 +431,23 @@ def main():
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
 
-    # The metric names 1500 B AND 9000 B frames: the second frame size is timed
-    # in the same run, same K / W / submission, and reported beside the first.
-    if args.also and args.also != args.config:
-        wl2 = build_workload(mi, synth, shard, args.also, 0, args.offs64, dev, rank, world)
-        wl2["name"] = args.also
+    # The metric names 1500 B AND 9000 B frames, and BASELINE.json lists 64 B
+    # minimum frames and the mixed-length Pareto batch: each is timed in the
+    # same run, same K / W / submission, same output check, and reported
+    # beside the headline with its own roofline.
+    for also in args.also:
+        wl2 = build_workload(mi, synth, shard, also, 0, args.offs64, dev, rank, world, args.outputs)
+        wl2["name"] = also
         m2 = measure(mi, shard, wl2, args, K, dev, dist, backend)
-        result[f"config_{args.also}"] = dict(value=m2["value"], unit="GiB/s", ms_per_step=m2["ms_per_step"],
-                                             mpkt_per_s=m2["mpkt_per_s"], workload=m2["config"]["workload"],
-                                             rotating_batches=m2["config"]["rotating_batches"],
-                                             roofline=m2["roofline"])
-        del wl2
+        row = dict(value=m2["value"], unit="GiB/s", ms_per_step=m2["ms_per_step"],
+                   mpkt_per_s=m2["mpkt_per_s"], scaling=wl2["scaling"], workload=m2["config"]["workload"],
+                   rotating_batches=m2["config"]["rotating_batches"], roofline=m2["roofline"],
+                   timed_outputs_checked=m2["timed_outputs"]["checked"],
+                   datagrams_checked=m2["timed_outputs"]["datagrams_checked"])
+        per_config_extras(row, also, m2)
+        result[f"config_{also}"] = row
+        result["timed_outputs_checked"] = result["timed_outputs_checked"] and m2["timed_outputs"]["checked"]
+        del wl2, m2
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
 

@@ -229,17 +229,10 @@ __device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint3
 }
 
 // The fields as byte stores (any layout; each store dirties part of a line).
-// MI_TX_STORE_EXP (compile-time, experiments only): 1 = skip the stores,
-// 2 = nontemporal, 3 = sc0 sc1 (write-through).
-#ifndef MI_TX_STORE_EXP
-#define MI_TX_STORE_EXP 0
-#endif
+// Default cache policy: nontemporal and write-through patch stores measured
+// slower (profiles/finalize_nt_ab_r02.jsonl, ceiling_writes_split_r02.jsonl).
 __device__ __forceinline__ void store_patch_bytes(__amdgpu_buffer_rsrc_t r, uint32_t off, const TxPatch &tp) {
-#if MI_TX_STORE_EXP == 1
-  if (tp.n == 7u) __builtin_amdgcn_raw_buffer_store_b8(0, r, off, 0, 0);  // never: keeps tp live
-  return;
-#endif
-  constexpr int aux = MI_TX_STORE_EXP == 2 ? 2 : MI_TX_STORE_EXP == 3 ? 17 : 0;
+  constexpr int aux = 0;
   if (tp.n > 0) {
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)tp.val0, r, off + tp.at0, 0, aux);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(tp.val0 >> 8), r, off + tp.at0 + 1u, 0, aux);
@@ -328,11 +321,7 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 #ifndef MI_RUN_CAPTURE
 #define MI_RUN_CAPTURE 1  // flat-run kernel: header windows from the streamed passes (0: reload them)
 #endif
-#ifdef MI_EXP_LB
-#define PACKED_BOUNDS __launch_bounds__(kBlock, MI_EXP_LB)
-#else
 #define PACKED_BOUNDS __launch_bounds__(kBlock)
-#endif
 // MODE: 0 RX verify; 1 TX finalize in place (finalize_store); 2 span folds
 // (mi_cksum_span_batch: out = ip_out, in_cksum_skip / pseudo-header seeds).
 template <int U, int MODE = 0>
@@ -954,9 +943,6 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_verify_slot64(Desc d, uint16_t 
 #ifndef MI_TX_FIRST_AUX
 #define MI_TX_FIRST_AUX 2
 #endif
-#if MI_TX_STORE_EXP == 4
-__device__ uint32_t g_tx_sink[1u << 22];
-#endif
 // Private-segment rule: every kernel in this file runs without scratch (the
 // CPU test test_no_kernel_uses_scratch reads the code object metadata).  The
 // round-2 variant of this kernel deferred its stores through state captured by
@@ -978,23 +964,15 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_finalize(Desc d) {
     const bool demux = d.flags & MI_BATCH_DEMUX;
     const bool odd = ((uintptr_t)d.base + off) & 1u;
     u32x4 h0 = v[0];  // pass 0, u = 0: chunk `lane` of the envelope (whole-block stores)
-#ifdef MI_TX_VERIFY_SUMS
-    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux);
-#else
     ipv4_sums<G, U, true>(r, off, flen, lane, v, ih, hdr_ok, do_l4, sum_h, sum_l, demux);
-#endif
     if constexpr (!BLOCKS) {
-#if MI_TX_STORE_EXP == 4
-      if (lane == 0) {
-        const TxPatch tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
-        g_tx_sink[i & ((1u << 22) - 1)] = tp.val0 ^ (tp.val1 << 16) ^ tp.n;
-      }
-#else
       if (lane == 0) store_patch_bytes(r, off, finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l));
-#endif
       (void)h0;
     } else {
-      TxPatch tp;
+      // lane 0 plans (its sums are the group's); the other lanes keep the
+      // value-initialised plan (TxPatch's members default to 0), so every
+      // lane's fields are defined before group_lane reads lane 0's
+      TxPatch tp{};
       if (lane == 0) tp = finalize_plan(r, off, flen, odd, ih, hdr_ok, do_l4, demux, sum_h, sum_l);
       const uint32_t n = group_lane<G>(tp.n, 0u);
       const uint32_t at0 = group_lane<G>(tp.at0, 0u), at1 = group_lane<G>(tp.at1, 0u);
@@ -1378,9 +1356,6 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
 // piece of a segment is read as the two aligned source chunks around it and
 // funnel-shifted (v_alignbyte) into destination alignment; bytes outside the
 // piece are masked off.
-#ifndef TX_WAVES
-#define TX_WAVES 1
-#endif
 struct TxDesc {
   const uint8_t *src;
   uint32_t src_bytes;
@@ -1604,15 +1579,9 @@ constexpr int kTxSeg = 4;
 __device__ __forceinline__ u32x4 ld16_src(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MI_TX_LOAD_AUX);
 }
-// MI_TX_PIPE=1: the frame's passes software-pipelined (below).  Measured on
-// MI355X (profiles/tx_pipe_r02.jsonl, same box, interleaved): socket frames
-// 57.9 us per launch against 51.3 one pass at a time, single-segment frames
-// 55.2 vs 48.3 -- the second pass of loads pushes the 128-VGPR bound into
-// 52 B/lane of scratch spills and the per-chunk cut is computed twice -- so
-// it is off.
-#ifndef MI_TX_PIPE
-#define MI_TX_PIPE 0
-#endif
+// (A software-pipelined variant -- pass p+1's loads issued before pass p is
+// built -- measured slower: the second register set spilled at the 128-VGPR
+// bound, socket frames 57.9 vs 51.3 us; profiles/tx_pipe_r02.jsonl.)
 
 // A frame's first kTxSeg nonempty segments: segment e covers frame bytes
 // [S_e, S_e+1) (S_0 = 0, the last one to L), frame byte q of segment e sits
@@ -1920,38 +1889,6 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
       const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
       u32x4 held{0, 0, 0, 0};
-#if MI_TX_PIPE
-      // Software pipeline over the frame's passes: pass p+1's loads are issued
-      // before pass p is built, folded and stored, so a group keeps a pass of
-      // loads in flight while it computes (the kernel waited on memory 53 % of
-      // its wave cycles with one pass at a time, profiles/pmc_tx_shapes_r02.jsonl).
-      // The cut of a chunk is recomputed at build time instead of being held
-      // (registers: U <= 2 shapes are bounded to 128).  Past the last pass
-      // the loads get the out-of-range offset (no traffic).
-      u32x4 xa[U], xb[U];
-      auto issue = [&](uint32_t p, u32x4 (&a)[U], u32x4 (&b)[U]) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
-          const bool in = p < npass && !c.slow;
-          a[u] = ld16_src(rs, in && c.q0 < sg.L ? c.A1 : kOOB);
-          b[u] = ld16_src(rs, in && c.two ? c.A2 : kOOB);
-        }
-      };
-      issue(0, xa, xb);
-      for (uint32_t p = 0; p < npass; ++p) {
-        u32x4 v[U];
-        u32x4 ya[U], yb[U];
-        issue(p + 1, ya, yb);
-        if (p == 0) prefetch2();
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          xa[u] = ya[u];
-          xb[u] = yb[u];
-        }
-#else
       for (uint32_t p = 0; p < npass; ++p) {
         u32x4 v[U];
         u32x4 xa[U], xb[U];
@@ -1966,7 +1903,6 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         if (p == 0) prefetch2();
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
-#endif
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
@@ -2006,9 +1942,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
     }
     prefetch2();
-#ifndef TX_NO_GENERIC
     if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
-#endif
   }
 }
 
@@ -2213,6 +2147,7 @@ void ctx_release(ThreadCtx &c, int back) {
 }
 
 void thread_exit_register();
+bool retire_dropins();
 
 // Make sure the calling thread has a context on its current HIP device.
 int ensure_ctx() {
@@ -2223,8 +2158,11 @@ int ensure_ctx() {
   int rc = check_device(dev);
   if (rc) return rc;
   if (t_ctx.device != -1) {
-    // thread moved to another device: release the old context's streams,
-    // events and buffers on the device they belong to, then start afresh
+    // thread moved to another device: retire its drop-in dispatches (they
+    // read the staging buffer and write the result word), then release the
+    // old context's streams, events and buffers on the device they belong to,
+    // and start afresh
+    retire_dropins();
     ctx_release(t_ctx, dev);
     t_ctx = ThreadCtx();
   }
@@ -2430,7 +2368,11 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
     return {kPlanSlot64, {0, 0}, 0};
   if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
     Plan pl{kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
-    if ((d.flags & MI_BATCH_PACKED) && d.offs && !pu_env && run_dma_code() > 0) pl.dma = run_dma_code();
+    // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
+    // offset / length arrays: batches whose arrays reach kOOB take the register
+    // kernel, whose descriptor reads are 64-bit)
+    if ((d.flags & MI_BATCH_PACKED) && d.offs && !pu_env && run_dma_code() > 0 && (uint64_t)d.n * 8u < kOOB)
+      pl.dma = run_dma_code();
     return pl;
   }
   if (!d.lens || g_tune.g || max_len < kClassEdges[1]) return {kPlanShape, pick_shape(max_len), 0};
@@ -2685,8 +2627,12 @@ struct AqlDevice {
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
-// HSA queues the library holds right now (diagnostics: mi_cksum_hsa_queues)
+// HSA queues the library holds right now (diagnostics: mi_cksum_hsa_queues),
+// and those it gave up on: a thread's queue whose last dispatch never retired
+// (a GPU fault or hang) is leaked with everything the dispatch may still touch,
+// counted here instead of in g_live_queues (mi__hsa_queues_leaked)
 std::atomic<int> g_live_queues{0};
+std::atomic<int> g_leaked_queues{0};
 
 // Every library-owned HSA queue reports its errors into the slot of the object
 // that owns it (an AqlRun or a thread's AqlOne), passed as the callback data:
@@ -3134,7 +3080,11 @@ struct AqlOne {
   uint8_t *karg = nullptr;  // page-locked, mapped: kAqlOneSlots blocks of 512 B
   uint32_t next = 0;
   bool unretired = false;   // unsignalled dispatches whose retirement nobody has seen
-  std::atomic<int> err{0};  // the queue's error (aql_queue_error)
+  // the queue's error slot (aql_queue_error's callback data): on the heap, not
+  // in thread-local storage, so a queue leaked after a failed quiesce can still
+  // report into it after the thread has gone (it is leaked with the queue)
+  std::atomic<int> *err = nullptr;
+  int error() const { return err ? err->load() : 0; }
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
@@ -3144,7 +3094,7 @@ int aql_one_slot(AqlOne &o, uint64_t *idx, void **slot) {
   *idx = hsa_queue_add_write_index_screlease(o.q, 1);
   const double t0 = mono_s();
   while (*idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
-    if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
+    if (o.error()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.error());
     if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: queue full for 10 s");
   }
   *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (*idx & (o.q->size - 1));
@@ -3154,7 +3104,7 @@ int aql_one_slot(AqlOne &o, uint64_t *idx, void **slot) {
 int aql_one_wait(AqlOne &o) {
   const double t0 = mono_s();
   while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
-    if (o.err.load()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.err.load());
+    if (o.error()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.error());
     if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
   }
   return 0;
@@ -3180,13 +3130,29 @@ int aql_one_quiesce(AqlOne &o) {
   return 0;
 }
 
-void aql_one_release(AqlOne &o) {
-  // a dispatch that never retires keeps its queue, signal and argument slots
-  // (leaked rather than freed under a running kernel)
-  if (o.q && aql_one_quiesce(o) == 0) {
-    aql_queue_destroy(o.q);
-    if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
-    if (o.karg) (void)hipHostFree(o.karg);
+// Returns true when the queue had to be LEAKED: a dispatch on it never
+// retired (a GPU fault or a hang), so the queue, its signal, its argument
+// slots and error slot -- and, the caller's part, the scalar staging buffer
+// and result word that dispatch reads and writes -- are kept rather than
+// freed under a running kernel.  The reason is reported on stderr once per
+// leak and the queue moves from g_live_queues to g_leaked_queues.
+bool aql_one_release(AqlOne &o) {
+  bool leaked = false;
+  if (o.q) {
+    if (aql_one_quiesce(o) == 0) {
+      aql_queue_destroy(o.q);
+      if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
+      if (o.karg) (void)hipHostFree(o.karg);
+      delete o.err;
+    } else {
+      leaked = true;
+      g_live_queues.fetch_sub(1);
+      g_leaked_queues.fetch_add(1);
+      fprintf(stderr, "libmicksum: a dispatch on this thread's HSA queue never retired (%s); the queue and the "
+              "buffers it may still use are leaked, not freed\n", t_err);
+    }
+  } else {
+    delete o.err;
   }
   o.device = -1;
   o.dev = nullptr;
@@ -3195,15 +3161,27 @@ void aql_one_release(AqlOne &o) {
   o.karg = nullptr;
   o.next = 0;
   o.unretired = false;
-  o.err.store(0);
+  o.err = nullptr;
+  return leaked;
 }
 
 // Thread exit: a thread that used the library gives back its HSA queue,
 // signal, argument slots, streams and buffers (a pthread key destructor --
 // these run when a thread ends, not for the main thread at process exit,
 // when the runtime is being torn down anyway).
+// Retire the thread's drop-in dispatches before anything they use is freed;
+// if one never retires, its staging buffer and result word are leaked with
+// its queue (ctx_release then skips them).
+bool retire_dropins() {
+  if (!aql_one_release(t_aql1)) return false;
+  t_ctx.stage = t_ctx.stage_dev = nullptr;
+  t_ctx.stage_cap = 0;
+  t_ctx.sout = t_ctx.sout_dev = nullptr;
+  return true;
+}
+
 void thread_exit_cleanup(void *) {
-  aql_one_release(t_aql1);
+  retire_dropins();
   if (t_ctx.device != -1) {
     ctx_release(t_ctx, t_ctx.device);
     t_ctx = ThreadCtx();
@@ -3223,10 +3201,11 @@ void thread_exit_register() {
 int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait) {
   AqlOne &o = t_aql1;
   if (o.device != t_ctx.device) {
-    aql_one_release(o);
+    if (aql_one_release(o)) return set_err(-EIO, "AQL engine: the thread's previous queue never retired");
     int rc = aql_device(t_ctx.device, &o.dev);
     if (rc) return rc;
-    if ((rc = aql_queue_create(o.dev->agent, 64, &o.err, &o.q))) return rc;
+    o.err = new std::atomic<int>(0);
+    if ((rc = aql_queue_create(o.dev->agent, 64, o.err, &o.q))) return rc;
     if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
       aql_one_release(o);
       return set_err(-EIO, "AQL engine: hsa_signal_create failed");
@@ -3277,6 +3256,9 @@ extern "C" {
 
 const char *mi_cksum_version(void) { return MI_CKSUM_VERSION; }
 int mi_cksum_hsa_queues(void) { return g_live_queues.load(); }
+// Diagnostics (not in the public header): queues leaked because a dispatch on
+// them never retired (aql_one_release).
+int mi__hsa_queues_leaked(void) { return g_leaked_queues.load(); }
 const char *mi_cksum_strerror(void) { return t_err; }
 
 int mi_cksum_device_count(void) {
@@ -4412,7 +4394,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
       // and the completion race)
       bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
       if (used_aql) {
-        if (t_aql1.err.load()) return set_err(-EIO, "scalar fold: queue error 0x%x", t_aql1.err.load());
+        if (t_aql1.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", t_aql1.error());
       } else {
         const hipError_t e = hipStreamQuery(c.sstream);
         if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));

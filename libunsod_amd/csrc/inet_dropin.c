@@ -38,7 +38,6 @@ struct mi_mbuf_view {
 _Static_assert(offsetof(struct mi_mbuf_view, m_data) == 16, "m_data@16 (mbuf.h:93)");
 _Static_assert(offsetof(struct mi_mbuf_view, m_len) == 24, "m_len@24 (mbuf.h:94)");
 
-/* Visit the (addr, len) spans in_cksum_skip would fold, in stream order. */
 static mi_cksum_error_fn g_dropin_handler;
 
 void mi_cksum_set_dropin_error_handler(mi_cksum_error_fn fn)
@@ -57,6 +56,7 @@ static uint16_t dropin_fail(const char *what)
 	return 0xffff;
 }
 
+/* Visit the (addr, len) spans in_cksum_skip would fold, in stream order. */
 static long walk_skip(const struct mi_mbuf_view *m, long len, long skip, uint8_t *dst)
 {
 	long total = 0, rem = len - skip;
