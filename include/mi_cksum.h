@@ -458,6 +458,22 @@ typedef struct mi_tx_batch {
 int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream);
 
 /*
+ * mi_cksum_tx_copy for frames in HOST memory -- the driver's real situation:
+ * the socket-buffer chains and the rte_mbuf data rooms are hugepage host
+ * memory (if_dpdk_transmit, uinet_if_dpdk.c:583-597).  b->src, b->dst, every
+ * descriptor array and status are host pointers; same rules, same bytes in
+ * the slots, same status as mi_cksum_tx_copy.  Synchronous.
+ *   zero-copy -- [src, src + src_bytes) and [dst, dst + dst_bytes) inside
+ *     ranges registered with mi_cksum_host_register: the kernel gathers the
+ *     chains over PCIe and writes the slots in place (descriptors and status
+ *     through mapped host memory: one dispatch, one wait);
+ *   staged -- otherwise, or with MI_TX_HOST_STAGED: source and slot region
+ *     copied to device memory and back around the same kernel.
+ */
+#define MI_TX_HOST_STAGED 1u
+int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags);
+
+/*
  * Host-resident batch (the path's real start and end: DPDK mbufs in host
  * memory).  b->base / offs / lens are HOST pointers; outputs are host arrays.
  * Synchronous: returns when outputs are written.  Two ways across PCIe:

@@ -338,6 +338,27 @@ def tx_copy(tb: TxBatch, *, status=None, stream=None):
     return status
 
 
+def tx_copy_host(src: np.ndarray, seg_off, seg_len, pkt_seg, pkt_len, dst: np.ndarray, *, dst_stride: int,
+                 dst_first: int = 0, room: int | None = None, l3_off: int = 14, csum_flags=None, csum_data=None,
+                 max_len: int = 0, staged: bool = False) -> np.ndarray:
+    """TX copy + sums for frames in host memory (mi_cksum_tx_copy_host): the
+    chains in the numpy blob ``src`` are copied into the slots of the numpy
+    buffer ``dst`` in place.  Zero-copy when both are registered with
+    ``host_register`` (and not ``staged``).  Returns the per-frame status."""
+    arr = {k: np.ascontiguousarray(v, dt) if v is not None else None
+           for k, v, dt in (("so", seg_off, np.uint64), ("sl", seg_len, np.int32), ("ps", pkt_seg, np.uint32),
+                            ("pl", pkt_len, np.uint32), ("cf", csum_flags, np.uint32), ("cd", csum_data, np.uint32))}
+    n = int(arr["pl"].size)
+    room = int(dst_stride) if room is None else int(room)
+    st = np.zeros(max(n, 1), np.uint8)
+    c = TxBatchC(src.ctypes.data, src.nbytes, arr["so"].ctypes.data, arr["sl"].ctypes.data, arr["ps"].ctypes.data,
+                 arr["pl"].ctypes.data, None if arr["cf"] is None else arr["cf"].ctypes.data,
+                 None if arr["cd"] is None else arr["cd"].ctypes.data, dst.ctypes.data, dst.nbytes, int(dst_stride),
+                 int(dst_first), room, int(l3_off), n, int(max_len))
+    check("mi_cksum_tx_copy_host", load().mi_cksum_tx_copy_host(C.byref(c), st.ctypes.data, 1 if staged else 0))
+    return st[:n]
+
+
 def ipv4_verify_repeat(batches, outs, steps: int, nstreams: int = 1, timing: str = "region",
                        graph: bool = False):
     """Launch ``steps`` verify passes back to back from native code: pass k over
@@ -520,5 +541,5 @@ __all__ = [
     "MbufChain", "in_cksum_skip", "in_cksum", "in_cksum_pseudo_header", "in_cksum_hdr", "in_pseudo",
     "in_addword", "PktBatch", "ipv4_verify", "ipv4_finalize", "span_batch", "synth_ipv4",
     "ipv4_verify_host", "ipv4_verify_multi", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "host_register", "host_unregister", "set_shape", "set_run_kernel", "set_busy_wait", "init", "device_count", "version",
-    "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy",
+    "MI_SPAN_STREAM", "MI_SPAN_ABS", "TxBatch", "tx_copy", "tx_copy_host",
 ]

@@ -207,7 +207,7 @@ __device__ __forceinline__ TxPatch finalize_plan(__amdgpu_buffer_rsrc_t r, uint3
     if (odd) sl = swap16(sl);
     uint32_t c = ~sl & 0xffffu;
     if (ih.proto == 17u && c == 0u) c = 0xffffu;
-    const uint32_t at = ih.hl + (ih.proto == 6u ? 16u : 6u);
+    const uint32_t at = ih.hl + (ih.proto == 6u ? MI_CSUM_DATA_TCP : MI_CSUM_DATA_UDP);
     if (at + 2u <= flen) tp.add(at, c);
   } else if (do_l4) {
     // ICMP / IGMP / CARP (demux): in_cksum over the message, sum field = 0
@@ -1665,7 +1665,7 @@ __device__ __forceinline__ TxPlan tx_plan(const TxDesc &t, uint32_t i, uint32_t 
   pl.do_ip = pl.ok && (fl & MI_CSUM_IP);
   pl.do_l4 = pl.ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
   pl.udp = fl & MI_CSUM_UDP;
-  pl.at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? 16u : 6u);
+  pl.at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? MI_CSUM_DATA_TCP : MI_CSUM_DATA_UDP);
   pl.hend = pl.ok ? (int)ih.hl : 0;
   pl.lend = pl.ok ? (int)ih.iplen : 0;
   return pl;
@@ -2071,6 +2071,9 @@ struct ThreadCtx {
   // zero-copy host path: descriptors / outputs in mapped host memory (grown on demand)
   uint8_t *zhost = nullptr, *zhost_dev = nullptr;
   size_t zhost_cap = 0;
+  // staged TX host path: source blob, slot region, descriptors (device)
+  uint8_t *tx_src = nullptr, *tx_dst = nullptr, *tx_desc = nullptr;
+  size_t tx_src_cap = 0, tx_dst_cap = 0, tx_desc_cap = 0;
   // repeat-launch streams and timing events
   static constexpr int kMaxRep = 8;
   hipStream_t rstream[kMaxRep] = {};
@@ -2131,6 +2134,9 @@ void ctx_release(ThreadCtx &c, int back) {
   }
   dfree(c.dbad);
   hfree(c.zhost);
+  dfree(c.tx_src);
+  dfree(c.tx_dst);
+  dfree(c.tx_desc);
   for (int q = 0; q < ThreadCtx::kMaxRep; ++q) {
     stream(c.rstream[q]);
     if (c.rjoin[q]) (void)hipEventDestroy(c.rjoin[q]);
@@ -3899,11 +3905,12 @@ int mi_cksum_set_busy_wait(int on) {
   return 0;
 }
 
-int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
-  int rc = ensure_ctx();
-  if (rc) return rc;
-  if (!b) return set_err(-EINVAL, "batch is NULL");
-  if (!b->n) return 0;
+}  // extern "C"
+
+namespace {
+// mi_tx_batch -> kernel descriptor, with the ABI's checks (pointers as given:
+// device pointers, or device views of host memory)
+int make_txdesc(const mi_tx_batch *b, uint8_t *status, TxDesc *out) {
   if (!b->src || !b->dst || !b->seg_off || !b->seg_len || !b->pkt_seg || !b->pkt_len || !status)
     return set_err(-EINVAL, "NULL array");
   if (((uintptr_t)b->src & 15u) || ((uintptr_t)b->dst & 15u))
@@ -3914,7 +3921,8 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
   if (last > b->dst_bytes)
     return set_err(-ERANGE, "slot %u ends at %llu > dst_bytes %llu", b->n - 1, (unsigned long long)last,
                    (unsigned long long)b->dst_bytes);
-  TxDesc t{};
+  TxDesc &t = *out;
+  t = TxDesc{};
   t.src = (const uint8_t *)b->src;
   t.src_bytes = (uint32_t)((b->src_bytes + 15u) & ~15ull);
   t.n = b->n;
@@ -3931,6 +3939,19 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
   t.dst_stride = b->dst_stride;
   t.dst_first = b->dst_first;
   t.status = status;
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (!b->n) return 0;
+  TxDesc t;
+  if ((rc = make_txdesc(b, status, &t))) return rc;
   return launch_tx(t, pick_tx_shape(b->max_len ? b->max_len : b->room), (hipStream_t)stream);
 }
 
@@ -4299,6 +4320,106 @@ int mi_cksum_rx_offload_host(const mi_pkt_batch *b, uint32_t *csum_flags, uint32
                              uint32_t *bad_count) {
   if (!csum_flags) return set_err(-EINVAL, "csum_flags is NULL");
   return host_batch(b, HostOut{nullptr, nullptr, nullptr, csum_flags, csum_data}, bad_count);
+}
+
+// TX copy + sums for frames in host memory (the driver's if_dpdk_transmit,
+// uinet_if_dpdk.c:583-597: socket-buffer chains -> hugepage rte_mbufs).
+int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!b) return set_err(-EINVAL, "batch is NULL");
+  if (!b->n) return 0;
+  if (!b->pkt_seg || !b->seg_off || !b->seg_len || !b->pkt_len || !status) return set_err(-EINVAL, "NULL array");
+  ThreadCtx &c = t_ctx;
+  const uint64_t n = b->n;
+  uint64_t nseg = 0;  // segments referenced: [0, max pkt_seg)
+  for (uint64_t i = 0; i <= n; ++i) nseg = b->pkt_seg[i] > nseg ? b->pkt_seg[i] : nseg;
+  // descriptor block: seg_off 8 nseg | seg_len 4 nseg | pkt_seg 4 (n + 1) | pkt_len 4 n | flags 4 n |
+  // data 4 n | status n
+  const size_t o_sl = 8 * nseg, o_ps = o_sl + 4 * nseg, o_pl = o_ps + 4 * (n + 1), o_cf = o_pl + 4 * n;
+  const size_t o_cd = o_cf + 4 * n, o_st = o_cd + 4 * n, need = o_st + n + 64;
+  auto fill = [&](uint8_t *h) {
+    memcpy(h, b->seg_off, 8 * nseg);
+    memcpy(h + o_sl, b->seg_len, 4 * nseg);
+    memcpy(h + o_ps, b->pkt_seg, 4 * (n + 1));
+    memcpy(h + o_pl, b->pkt_len, 4 * n);
+    if (b->csum_flags) memcpy(h + o_cf, b->csum_flags, 4 * n);
+    if (b->csum_data) memcpy(h + o_cd, b->csum_data, 4 * n);
+  };
+  auto view = [&](const uint8_t *z, const void *src, void *dst, mi_tx_batch *v) {
+    *v = *b;
+    v->src = src;
+    v->dst = dst;
+    v->seg_off = (const uint64_t *)z;
+    v->seg_len = (const int32_t *)(z + o_sl);
+    v->pkt_seg = (const uint32_t *)(z + o_ps);
+    v->pkt_len = (const uint32_t *)(z + o_pl);
+    v->csum_flags = b->csum_flags ? (const uint32_t *)(z + o_cf) : nullptr;
+    v->csum_data = b->csum_data ? (const uint32_t *)(z + o_cd) : nullptr;
+  };
+  if (!c.hstream[0])
+    for (int k = 0; k < ThreadCtx::kRing; ++k) HIP_TRY(hipStreamCreateWithFlags(&c.hstream[k], hipStreamNonBlocking));
+  hipStream_t st = c.hstream[0];
+  const Shape sh = pick_tx_shape(b->max_len ? b->max_len : b->room);
+  void *sdev = nullptr, *ddev = nullptr;
+  const bool zc = !(flags & MI_TX_HOST_STAGED) && b->src && b->dst && b->src_bytes && b->dst_bytes &&
+                  b->src_bytes <= kMaxBytes && b->dst_bytes <= kMaxBytes && host_range_mapped(b->src, b->src_bytes) &&
+                  host_range_mapped(b->dst, b->dst_bytes) &&
+                  hipHostGetDevicePointer(&sdev, const_cast<void *>(b->src), 0) == hipSuccess &&
+                  hipHostGetDevicePointer(&ddev, b->dst, 0) == hipSuccess && sdev && ddev;
+  (void)hipGetLastError();
+  if (zc) {
+    // zero-copy: descriptors and status through the mapped per-thread block
+    if (c.zhost_cap < need) {
+      if (c.zhost) HIP_TRY(hipHostFree(c.zhost));
+      c.zhost = c.zhost_dev = nullptr;
+      c.zhost_cap = 0;
+      size_t cap = 1u << 16;
+      while (cap < need) cap <<= 1;
+      HIP_TRY(hipHostMalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(hipHostGetDevicePointer((void **)&c.zhost_dev, c.zhost, 0));
+      c.zhost_cap = cap;
+    }
+    fill(c.zhost);
+    mi_tx_batch v;
+    view(c.zhost_dev, sdev, ddev, &v);
+    TxDesc t;
+    if ((rc = make_txdesc(&v, c.zhost_dev + o_st, &t))) return rc;
+    if ((rc = launch_tx(t, sh, st))) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(status, c.zhost + o_st, n);
+    return 0;
+  }
+  // staged: the source blob and the whole slot region go to device memory and
+  // the slot region comes back (bytes no frame writes return unchanged)
+  if (!b->src || !b->dst) return set_err(-EINVAL, "NULL array");
+  auto grow = [&](uint8_t *&p, size_t &cap, size_t want) -> int {
+    if (cap >= want) return 0;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc((void **)&p, want));
+    cap = want;
+    return 0;
+  };
+  const size_t sbytes = (b->src_bytes + 15u) & ~15ull, dbytes = (b->dst_bytes + 15u) & ~15ull;
+  if ((rc = grow(c.tx_src, c.tx_src_cap, sbytes + 16)) || (rc = grow(c.tx_dst, c.tx_dst_cap, dbytes + 16)) ||
+      (rc = grow(c.tx_desc, c.tx_desc_cap, need)))
+    return rc;
+  std::vector<uint8_t> hd(need);
+  fill(hd.data());
+  HIP_TRY(hipMemcpyAsync(c.tx_src, b->src, b->src_bytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c.tx_dst, b->dst, b->dst_bytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(c.tx_desc, hd.data(), need, hipMemcpyHostToDevice, st));
+  mi_tx_batch v;
+  view(c.tx_desc, c.tx_src, c.tx_dst, &v);
+  TxDesc t;
+  if ((rc = make_txdesc(&v, c.tx_desc + o_st, &t))) return rc;
+  if ((rc = launch_tx(t, sh, st))) return rc;
+  HIP_TRY(hipMemcpyAsync(b->dst, c.tx_dst, b->dst_bytes, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipMemcpyAsync(status, c.tx_desc + o_st, n, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return 0;
 }
 
 // ---------------------------------------------------------- (b1) scalar bridge
