@@ -324,20 +324,23 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 #define PACKED_BOUNDS __launch_bounds__(kBlock)
 // MODE: 0 RX verify; 1 TX finalize in place (finalize_store); 2 span folds
 // (mi_cksum_span_batch: out = ip_out, in_cksum_skip / pseudo-header seeds).
-template <int U, int MODE = 0>
+// NW: waves per workgroup (each wave owns its own 64-datagram ranges and LDS
+// rows; a smaller workgroup frees its LDS as soon as its own waves are done,
+// not when the slowest of four heavy-tailed ranges is).
+template <int U, int MODE = 0, int NW = kBlock / 64>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes) {
   constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
-  __shared__ uint32_t s_q[kBlock / 64][W];
+  __shared__ uint32_t s_q[NW][W];
 #if MI_RUN_CAPTURE
-  __shared__ u32x4 s_c[kBlock / 64][W];  // the pass's chunks: header windows / last chunks come from here
+  __shared__ u32x4 s_c[NW][W];  // the pass's chunks: header windows / last chunks come from here
 #endif
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t rstride = gridDim.x * (kBlock / 64) * 64u;
+  const uint32_t rstride = gridDim.x * NW * 64u;
   uint32_t *sq = s_q[wv];
-  uint32_t p0 = (blockIdx.x * (kBlock / 64) + wv) * 64u;
+  uint32_t p0 = (blockIdx.x * NW + wv) * 64u;
   if (p0 >= d.n) return;
   // descriptors of this lane's datagram; the next range's are fetched while
   // this range is folded
@@ -520,10 +523,11 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
     verify_emit(pend, ip_out, l4_out, st_out, bad, d);
   }
 }
-template <int U, int MODE = 0>
-__global__ PACKED_BOUNDS void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
-                                                   uint32_t *bad, SpanSeeds sp, uint32_t abs_lanes) {
-  packed_body<U, MODE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+template <int U, int MODE = 0, int NW = kBlock / 64>
+__global__ __launch_bounds__(64 * NW) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                                uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
+                                                                uint32_t abs_lanes) {
+  packed_body<U, MODE, NW>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
 
 // The bounds of a wave's 64-datagram range (the flat-run kernels): the run
@@ -1966,6 +1970,16 @@ constexpr int kScalarThreads = 512;
   }
 #define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12) X(64, 4)
 MI_AQL_SHAPES(MI_AQL_SHAPE)
+// (the flat run with 1- and 2-wave workgroups: mi_aql_run<U>w<NW>)
+#define MI_AQL_RUN_W(U_, NW_)                                                                           \
+  extern "C" __global__ __launch_bounds__(64 * NW_) void mi_aql_run##U_##w##NW_(                        \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
+    packed_body<U_, 0, NW_>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                                       \
+  }
+MI_AQL_RUN_W(4, 1)
+MI_AQL_RUN_W(4, 2)
+MI_AQL_RUN_W(8, 1)
+MI_AQL_RUN_W(8, 2)
 #define MI_AQL_RUN(U_)                                                                                  \
   extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
                                                            uint32_t *bad) {                             \
@@ -2326,6 +2340,7 @@ struct Plan {
   PlanKind kind;
   Shape shape;  // kPlanShape
   int run_u;    // kPlanRun: chunks per lane per pass
+  int run_nw = 4;  // kPlanRun: waves per workgroup (k_ipv4_verify_packed<U, 0, NW>)
   int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
 };
 
@@ -2354,6 +2369,20 @@ int run_dma_code() {
   return c;
 }
 
+// Waves per workgroup of the flat-run verify (MI_CKSUM_RUN_WAVES = 1, 2 or 4;
+// mi__set_run_waves for tests).
+std::atomic<int> g_run_waves{0};
+int run_waves() {
+  int w = g_run_waves.load(std::memory_order_relaxed);
+  if (!w) {
+    const char *e = getenv("MI_CKSUM_RUN_WAVES");
+    const int v = e ? atoi(e) : 0;
+    w = v == 1 || v == 2 ? v : 4;
+    g_run_waves.store(w, std::memory_order_relaxed);
+  }
+  return w;
+}
+
 Plan verify_plan(const Desc &d, uint32_t max_len) {
   // chunks per lane per pass of the flat-run kernel: 8 for packed mixed
   // lengths, 4 for dense minimum-size slots (profiles/packed_u_r01.jsonl);
@@ -2374,6 +2403,7 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
     return {kPlanSlot64, {0, 0}, 0};
   if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
     Plan pl{kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
+    pl.run_nw = pl.run_u == 16 ? 4 : run_waves();
     // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
     // offset / length arrays: batches whose arrays reach kOOB take the register
     // kernel, whose descriptor reads are 64-bit)
@@ -2386,14 +2416,15 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
 }
 
 // Grids of the flat-run and 64-byte-slot kernels: 64 datagrams per wave.
-unsigned run_blocks(const Desc &d) {
+unsigned run_blocks(const Desc &d, int nw = 4) {
   static const int run_cap = [] {
     const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 16384;
   }();
-  const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap;
-  uint64_t blocks = ((uint64_t)d.n + 255) / 256;
+  // (the cap counts 4-wave workgroups' worth of waves)
+  const int cap = (g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap) * (4 / nw);
+  uint64_t blocks = ((uint64_t)d.n + 64u * nw - 1) / (64u * nw);
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
 }
@@ -2432,6 +2463,16 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     return launched();                                                                                       \
   }
     MI_RUN_DMA_SHAPES(X)
+#undef X
+  }
+  if (pl.kind == kPlanRun && pl.run_nw != 4) {
+    const dim3 grid(run_blocks(d, pl.run_nw)), blk(64 * pl.run_nw);
+#define X(U_, NW_)                                                                                           \
+  if (pl.run_u == U_ && pl.run_nw == NW_) {                                                                  \
+    VLAUNCH((k_ipv4_verify_packed<U_, 0, NW_>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);         \
+    return launched();                                                                                       \
+  }
+    X(4, 1) X(4, 2) X(8, 1) X(8, 2)
 #undef X
   }
   if (pl.kind == kPlanRun) {
@@ -2583,7 +2624,7 @@ enum AqlKernelId {
 #define X(G_, U_) kAqlV_##G_##x##U_,
   MI_AQL_SHAPES(X)
 #undef X
-  kAqlRun4, kAqlRun8, kAqlRun16,
+  kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2593,7 +2634,7 @@ const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
     MI_AQL_SHAPES(X)
 #undef X
-    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16",
+    "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2602,7 +2643,8 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
 #undef X
-    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16,
+    (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
+    (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2808,8 +2850,10 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
 #undef X
   }
   if (pl.kind == kPlanRun) {
-    *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
-    *blocks = run_blocks(d);
+    if (pl.run_nw == 1) *id = pl.run_u == 4 ? kAqlRun4w1 : kAqlRun8w1;
+    else if (pl.run_nw == 2) *id = pl.run_u == 4 ? kAqlRun4w2 : kAqlRun8w2;
+    else *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
+    *blocks = run_blocks(d, pl.run_nw);
     return 0;
   }
   if (pl.kind == kPlanSlot64) {
@@ -2886,9 +2930,18 @@ void aql_fill_raw(uint8_t *ka, const void *args, uint32_t nargs, unsigned blocks
   memcpy(h + 18, rem, sizeof rem);
   memcpy(h + 64, &dims, sizeof dims);
 }
-void aql_fill_args(uint8_t *ka, const AqlArgs &args, unsigned blocks) {
+// Workgroup size of each entry point (its __launch_bounds__).
+unsigned aql_wg(int id) {
+  switch (id) {
+    case kAqlRun4w1: case kAqlRun8w1: return 64;
+    case kAqlRun4w2: case kAqlRun8w2: return 128;
+    case kAqlScalar: return kScalarThreads;
+    default: return kBlock;
+  }
+}
+void aql_fill_args(uint8_t *ka, const AqlArgs &args, unsigned blocks, unsigned wg) {
   static_assert(kAqlHidden == ((sizeof(AqlArgs) + 7u) & ~7u), "hidden arguments follow the explicit ones");
-  aql_fill_raw(ka, &args, sizeof args, blocks, kBlock, ~0u);
+  aql_fill_raw(ka, &args, sizeof args, blocks, wg, ~0u);
 }
 // A dispatch packet without its header (written last, at submission).
 void aql_fill_packet(hsa_kernel_dispatch_packet_t &p, const AqlKernel &k, unsigned blocks, void *kargs,
@@ -2936,8 +2989,9 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
   }
   for (uint32_t j = 0; j < nb; ++j) {
     aql_fill_args(host.data() + (size_t)slot * j,
-                  AqlArgs{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr}, blocks[j]);
-    aql_fill_packet(a->pkt[j], dv->k[ids[j]], blocks[j], a->kargs + (size_t)slot * j);
+                  AqlArgs{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr}, blocks[j],
+                  aql_wg(ids[j]));
+    aql_fill_packet(a->pkt[j], dv->k[ids[j]], blocks[j], a->kargs + (size_t)slot * j, aql_wg(ids[j]));
   }
   e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -3265,6 +3319,13 @@ int mi_cksum_hsa_queues(void) { return g_live_queues.load(); }
 // Diagnostics (not in the public header): queues leaked because a dispatch on
 // them never retired (aql_one_release).
 int mi__hsa_queues_leaked(void) { return g_leaked_queues.load(); }
+// Diagnostics / tests (not in the public header): waves per workgroup of the
+// flat-run verify kernel (1, 2, 4; speed only, never results).
+int mi__set_run_waves(int w) {
+  if (w != 1 && w != 2 && w != 4) return set_err(-EINVAL, "run waves %d", w);
+  g_run_waves.store(w);
+  return 0;
+}
 const char *mi_cksum_strerror(void) { return t_err; }
 
 int mi_cksum_device_count(void) {
@@ -3450,7 +3511,8 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
   if (pl.kind == kPlanRun && pl.dma)
     snprintf(buf, sizeof buf, "k_ipv4_verify_run_dma<%d,%d>", pl.dma / 10, pl.dma % 10);
   else if (pl.kind == kPlanRun)
-    snprintf(buf, sizeof buf, "k_ipv4_verify_packed<%d>", pl.run_u);
+    snprintf(buf, sizeof buf, pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>" : "k_ipv4_verify_packed<%d,%d waves>",
+             pl.run_u, pl.run_nw);
   else if (pl.kind == kPlanShape)
     snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);
   else if (pl.kind == kPlanSlot64)
@@ -4118,7 +4180,7 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
       (wide ? aql_kernel_for_shape(d, Shape{64, 4}, &id, &blocks)
                         : aql_kernel_for(d, max_len, &id, &blocks)) == 0) {
     const AqlArgs args{d, zip, zl4, zst, zbad};
-    int rc = aql_one_submit(id, blocks, kBlock, &args, sizeof args, true);
+    int rc = aql_one_submit(id, blocks, aql_wg(id), &args, sizeof args, true);
     if (rc) return rc;
   } else {
     int rc = wide ? launch_verify_shape(d, Shape{64, 4}, zip, zl4, zst, zbad, st)
