@@ -120,6 +120,18 @@ __device__ __forceinline__ uint32_t group_scan(uint32_t x) {
   return x;
 }
 
+// Inclusive prefix sum over the wave: row shifts inside 16-lane rows, then
+// the row_bcast:15 / row_bcast:31 carries across rows.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return x;
+}
+
 struct Desc {
   const uint8_t *base;
   uint32_t bytes;  // bounds-check size (rounded up to 16)

@@ -275,17 +275,6 @@ __device__ __forceinline__ void span_store(uint32_t i, uint32_t off, uint32_t le
   out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
 }
 
-// Inclusive prefix sum over the wave: row shifts inside 16-lane rows, then
-// the row_bcast:15 / row_bcast:31 carries across rows.
-__device__ __forceinline__ uint32_t wave_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
-  return x;
-}
 
 // Sum over the wave, uniform (every lane gets it).
 __device__ __forceinline__ uint32_t wave_sum(uint32_t x) { return group_sum<64>(x); }
@@ -1338,617 +1327,7 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
   }
 }
 
-// ------------------------------------------- TX: fused copy + checksum offload
-//
-// SURVEY.md 8(f) rank 2.  With if_hwassist = CSUM_IP | CSUM_TCP | CSUM_UDP the
-// stack leaves the sums to the device (ip_output.c:649-672) and the driver
-// copies every outgoing frame out of its mbuf chain into an rte_mbuf
-// (m_copydata(m, 0, len, rm_data), uinet_if_dpdk.c:594-597).  Here both are
-// one pass: a lane group per frame gathers the chain into 16-byte chunks
-// aligned to the DESTINATION slot (so stores are whole dwordx4 except at the
-// frame's two ends), folds the IP header and the L4 range from those same
-// registers, patches ip_sum and the L4 sum field (in_delayed_cksum,
-// ip_output.c:958-983: UDP 0 -> 0xffff, stored only if it lies inside the IP
-// mbuf's m_len) into the chunk registers, and stores.  Read L, write L.
-//
-// Gather: lane j of the group builds destination chunk ci = p*G*U + u*G + j.
-// The segment table (m_data, m_len of each mbuf of the chain) sits one
-// segment per lane; a group scan turns lengths into frame positions.  For each
-// chunk the lane keeps the segment holding its first byte ("prim") and, when
-// the chunk straddles a segment boundary, the next non-empty one ("sec"); a
-// chunk touching three or more segments (tiny mbufs) takes a slow loop.  A
-// piece of a segment is read as the two aligned source chunks around it and
-// funnel-shifted (v_alignbyte) into destination alignment; bytes outside the
-// piece are masked off.
-struct TxDesc {
-  const uint8_t *src;
-  uint32_t src_bytes;
-  uint32_t n;
-  const uint64_t *seg_off;
-  const int32_t *seg_len;
-  const uint32_t *pkt_seg;
-  const uint32_t *pkt_len;
-  const uint32_t *cflags, *cdata;
-  uint8_t *dst;
-  uint32_t dst_bytes;
-  uint32_t room, l3;
-  uint64_t dst_stride, dst_first;
-  uint8_t *status;
-};
-
-// The 16 bytes at source address a (any alignment): the aligned chunk at
-// a & ~15 and (unless aligned) the next one, funnel-shifted.
-struct Raw2 {
-  u32x4 x, y;
-};
-__device__ __forceinline__ Raw2 ld_pair(__amdgpu_buffer_rsrc_t r, uint32_t a) {
-  const uint32_t A = a & ~15u;
-  return {ld16(r, A), ld16(r, (a & 15u) ? A + 16u : kOOB)};
-}
-__device__ __forceinline__ u32x4 shift2(const u32x4 &x, const u32x4 &y, uint32_t a) {
-  // named registers and selects only: an array here gets a select-of-index
-  // turned into a dynamic (scratch) access by the optimiser
-  const uint32_t s = a & 15u, b = s & 3u;
-  const bool h8 = s & 8u, h4 = s & 4u;
-  const uint32_t t0 = h8 ? x.z : x.x, t1 = h8 ? x.w : x.y, t2 = h8 ? y.x : x.z;
-  const uint32_t t3 = h8 ? y.y : x.w, t4 = h8 ? y.z : y.x, t5 = h8 ? y.w : y.y;
-  const uint32_t z0 = h4 ? t1 : t0, z1 = h4 ? t2 : t1, z2 = h4 ? t3 : t2;
-  const uint32_t z3 = h4 ? t4 : t3, z4 = h4 ? t5 : t4;
-  return {__builtin_amdgcn_alignbyte(z1, z0, b), __builtin_amdgcn_alignbyte(z2, z1, b),
-          __builtin_amdgcn_alignbyte(z3, z2, b), __builtin_amdgcn_alignbyte(z4, z3, b)};
-}
-__device__ __forceinline__ u32x4 shift_pair(const Raw2 &p, uint32_t a) { return shift2(p.x, p.y, a); }
-// Bytes [a, b) of a dword as a mask, 0 <= a, b <= 4 (32-bit shifts only).
-__device__ __forceinline__ uint32_t byte_mask(int a, int b) {
-  const uint32_t lo = a >= 4 ? 0u : 0xffffffffu << (8 * a);
-  const uint32_t hi = b >= 4 ? 0xffffffffu : ~(0xffffffffu << (8 * b));
-  return lo & hi;
-}
-// acc |= bytes [lo, hi) of chunk v (any lo, hi; clamped to the chunk)
-__device__ __forceinline__ void merge_bytes(u32x4 &acc, const u32x4 &v, int lo, int hi) {
-  if (lo <= 0 && hi >= 16) {
-    acc.x |= v.x; acc.y |= v.y; acc.z |= v.z; acc.w |= v.w;
-    return;
-  }
-  acc.x |= v.x & byte_mask(min(max(lo, 0), 4), min(max(hi, 0), 4));
-  acc.y |= v.y & byte_mask(min(max(lo - 4, 0), 4), min(max(hi - 4, 0), 4));
-  acc.z |= v.z & byte_mask(min(max(lo - 8, 0), 4), min(max(hi - 8, 0), 4));
-  acc.w |= v.w & byte_mask(min(max(lo - 12, 0), 4), min(max(hi - 12, 0), 4));
-}
-// Byte b (0..15) of chunk v := x, if 0 <= b < 16.
-__device__ __forceinline__ void put_byte(u32x4 &v, int b, uint32_t x) {
-  if (b < 0 || b >= 16) return;
-  const uint32_t sh = 8u * (b & 3), m = ~(0xffu << sh), y = (x & 0xffu) << sh;
-  const int j = b >> 2;
-  v.x = j == 0 ? (v.x & m) | y : v.x;
-  v.y = j == 1 ? (v.y & m) | y : v.y;
-  v.z = j == 2 ? (v.z & m) | y : v.z;
-  v.w = j == 3 ? (v.w & m) | y : v.w;
-}
-// Store bytes [lo, hi) of chunk v at destination address a (16-aligned).
-// Copied frames are written once and not read back by this kernel:
-// nontemporal stores (aux = 2, `nt`) lift a plain slot copy of the TX
-// geometry from 0.51 to 0.62 of HBM (tools/ceiling_copy.py,
-// profiles/ceiling_copy_r02.jsonl).
-#ifndef MI_TX_STORE_AUX
-#define MI_TX_STORE_AUX 2
-#endif
-__device__ __forceinline__ void store_chunk(__amdgpu_buffer_rsrc_t r, uint32_t a, const u32x4 &v, int lo,
-                                            int hi) {
-  constexpr int kAux = MI_TX_STORE_AUX;
-  if (lo <= 0 && hi >= 16) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, a, 0, kAux);
-    return;
-  }
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int b0 = min(max(lo - 4 * j, 0), 4), b1 = min(max(hi - 4 * j, 0), 4);
-    if (b0 == 0 && b1 == 4) {
-      __builtin_amdgcn_raw_buffer_store_b32(w[j], r, a + 4u * j, 0, kAux);
-    } else {
-      for (int m = b0; m < b1; ++m)
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[j] >> (8 * m)), r, a + 4u * j + m, 0, kAux);
-    }
-  }
-}
-
-// TX sums from the group's absolute-lane accumulators (in_delayed_cksum's
-// in_cksum_skip(m, ip_len, hl) and in_cksum(m, hl) with ip_sum = 0), both
-// returned in every lane of the group.
-template <int G>
-__device__ __forceinline__ void tx_sums(uint32_t acc_t, uint32_t acc_h, uint32_t acc_f, int hend,
-                                        const IpHdr &ih, bool odd, bool udp, uint32_t &c_ip,
-                                        uint32_t &c_l4) {
-  const uint32_t total = group_sum<G>(acc_t);
-  uint32_t hdr, field;
-  if (hend > 20) {
-    hdr = group_sum<G>(acc_h);
-    field = group_sum<G>(acc_f);
-  } else if (hend) {
-    hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
-          abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
-    field = abs_halves(ih.w[2] & 0xffff0000u, odd);
-  } else {
-    hdr = field = 0u;
-  }
-  uint32_t sh = fold16(hdr - field), sl = fold16(total - hdr);
-  if (odd) {
-    sh = swap16(sh);
-    sl = swap16(sl);
-  }
-  c_ip = ~sh & 0xffffu;
-  c_l4 = ~sl & 0xffffu;
-  if (udp && c_l4 == 0u) c_l4 = 0xffffu;
-  c_ip = group_lane<G>(c_ip, 0);
-  c_l4 = group_lane<G>(c_l4, 0);
-}
-
-// Fold one chunk of an IPv4 datagram whose first byte is rel bytes after the
-// datagram start (fold_pass for a single chunk; bytes outside the piece the
-// chunk carries are zero, so whole-chunk arithmetic stays exact).
-__device__ __forceinline__ void fold_chunk(const u32x4 &v, int rel, int lend, int hend, bool opts,
-                                           uint32_t &acc_t, uint32_t &acc_h, uint32_t &acc_f) {
-  const bool pure = rel >= 0 && rel + 16 <= lend;
-  acc_t += pure ? sum4(v) : 0u;
-  if (!pure && rel < lend) acc_t += range_sum(v, rel, 0, lend);
-  if (opts && rel < hend) {
-    acc_h += range_sum(v, rel, 0, hend);
-    acc_f += range_sum(v, rel, 10, 12);
-  }
-}
-
-// x as held by the next lane of this lane's G-lane group (G = 8 or 16), or,
-// for the group's last lane, by the group's first lane of xn: DPP row shifts.
-template <int G>
-__device__ __forceinline__ uint32_t next_lane(uint32_t x, uint32_t xn, bool last) {
-  static_assert(G == 8 || G == 16, "row-local groups only");
-  const uint32_t in = dpp_all<0x101>(x);             // row_shl:1
-  const uint32_t ed = dpp_all<0x110 + (G - 1)>(xn);  // row_shr:G-1
-  return last ? ed : in;
-}
-template <int G>
-__device__ __forceinline__ u32x4 next_lane4(const u32x4 &x, const u32x4 &xn, bool last) {
-  return {next_lane<G>(x.x, xn.x, last), next_lane<G>(x.y, xn.y, last), next_lane<G>(x.z, xn.z, last),
-          next_lane<G>(x.w, xn.w, last)};
-}
-
-// A piece of one segment: destination chunks [cfirst, clast) carrying frame
-// bytes [pa, pe), the byte at frame position q read from source address q + del.
-struct Piece {
-  uint32_t cfirst, clast, del;
-  int pa, pe;
-};
-
-// Pass p of a piece: each lane loads ONE aligned source chunk per destination
-// chunk ci = cfirst + p*G*U + u*G + lane (source chunks are consecutive across
-// the group's lanes, like the destination chunks); x[U] is the chunk after
-// the pass, loaded by the group's last lane only.  A misaligned piece also
-// needs the source chunk of clast.
-template <int G, int U>
-__device__ __forceinline__ void load_pass(__amdgpu_buffer_rsrc_t rs, const Piece &pc, uint32_t p, int lane,
-                                          uint32_t h, u32x4 (&x)[U + 1]) {
-  const uint32_t cb = pc.cfirst + p * (G * U);
-  const uint32_t lim = pc.clast + (((pc.del - h) & 15u) ? 1u : 0u);
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint32_t ci = cb + u * G + lane;
-    x[u] = ld16(rs, ci < lim ? (16u * ci - h + pc.del) & ~15u : kOOB);
-  }
-  const uint32_t ci = cb + U * G;
-  x[U] = ld16(rs, lane == G - 1 && ci < lim ? (16u * ci - h + pc.del) & ~15u : kOOB);
-}
-// Destination chunk u of pass p, shifted into destination alignment (the
-// second source chunk is the next lane's, fetched with a DPP row shift) and
-// masked to the piece.
-template <int G, int U>
-__device__ __forceinline__ u32x4 make_chunk(const u32x4 (&x)[U + 1], int u, const Piece &pc, uint32_t p,
-                                            int lane, uint32_t h) {
-  const uint32_t ci = pc.cfirst + p * (G * U) + u * G + lane;
-  const int cs = (int)(16u * ci) - (int)h;
-  const bool last = lane == G - 1;
-  // (computed by every lane before the select: a ternary arm is evaluated only
-  // by the lanes that take it, and the DPP would read switched-off lanes)
-  const u32x4 nl = next_lane4<G>(x[u], x[u + 1 < U ? u + 1 : u], last);
-  const u32x4 nx = u + 1 < U ? nl : (last ? x[U] : nl);
-  u32x4 v{0, 0, 0, 0};
-  if (ci < pc.clast) merge_bytes(v, shift2(x[u], nx, (uint32_t)cs + pc.del), pc.pa - cs, pc.pe - cs);
-  return v;
-}
-
-// Fast path of k_tx_copy: chunk-major gather with unaligned loads.  Every
-// nonempty mbuf of the frame (at most kTxSeg of them: the header mbuf and the
-// payload's cluster pieces) is kept as (frame position, source - position) in
-// registers; destination chunk ci (frame bytes [q0, q0 + 16), q0 = 16 ci - h)
-// takes each overlapping segment's bytes with ONE 16-byte load at the
-// segment's source address of q0 (gfx950 buffer loads accept any byte
-// address, tools/unaligned_probe.hip) -- no funnel shifts, no neighbour-lane
-// exchange -- and all of a pass's loads are issued before any is used.  A
-// load that would start before the source buffer or run past its end takes a
-// per-byte path instead (the first / last bytes of the buffer only).
-constexpr int kTxSeg = 4;
-// The source loads of the TX gather.  A group's 16-byte loads start at any
-// byte, so each wave-instruction's window of a frame straddles one more
-// 128-byte line than it covers, and the next pass's window starts in that same
-// line: with nontemporal loads (which do not keep the line in L2) every such
-// line came from HBM twice -- 1.45x the algorithmic read bytes, from the
-// request-size counters (32 B x RDREQ_32B + 64 B x RDREQ_64B + 128 B x
-// RDREQ_128B; profiles/r03/pmc_reqsize_r03.jsonl).  With the default policy
-// (MI_TX_LOAD_AUX 0) the straddled line is an L2 hit: 1.15x, and socket frames
-// 51.5 -> 47.1 us per 65536 x 1514 B batch (0.48 -> 0.53 of 8 TB/s),
-// single-segment frames 48.1 -> 44.4 us (0.51 -> 0.56); profiles/r03/tx_r03.jsonl.
-#ifndef MI_TX_LOAD_AUX
-#define MI_TX_LOAD_AUX 0
-#endif
-__device__ __forceinline__ u32x4 ld16_src(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, MI_TX_LOAD_AUX);
-}
-// (A software-pipelined variant -- pass p+1's loads issued before pass p is
-// built -- measured slower: the second register set spilled at the 128-VGPR
-// bound, socket frames 57.9 vs 51.3 us; profiles/tx_pipe_r02.jsonl.)
-
-// A frame's first kTxSeg nonempty segments: segment e covers frame bytes
-// [S_e, S_e+1) (S_0 = 0, the last one to L), frame byte q of segment e sits
-// at source offset q + D_e.  A 16-byte load at source offset A (u32; a
-// negative offset wraps past lim) is inside the source buffer iff A <= lim.
-struct TxSegs {
-  int S1, S2, S3, L;
-  uint32_t D0, D1, D2, D3, lim;
-};
-// Destination chunk ci (frame bytes [q0, q0 + 16), q0 = 16 ci - h): bytes
-// [max(q0, 0), q0 + B) come from segment j (the one holding the first byte,
-// loaded at A1), [q0 + B, min(q0 + 16, L)) from segment j + 1 (at A2) when
-// `two`.  clip: the chunk is cut by the frame's ends.  slow: it touches three
-// segments or a load would leave the source buffer.
-struct TxCut {
-  int q0, B;
-  uint32_t A1, A2;
-  bool two, clip, slow;
-};
-__device__ __forceinline__ TxCut tx_cut(const TxSegs &g, uint32_t ci, uint32_t h) {
-  const int S1 = g.S1, S2 = g.S2, S3 = g.S3, L = g.L;
-  const uint32_t D0 = g.D0, D1 = g.D1, D2 = g.D2, D3 = g.D3;
-  TxCut c;
-  c.q0 = (int)(16u * ci) - (int)h;
-  const int q = max(c.q0, 0), hi = min(c.q0 + 16, L);
-  const bool j1 = q >= S1, j2 = q >= S2, j3 = q >= S3;
-  const uint32_t d0 = j3 ? D3 : j2 ? D2 : j1 ? D1 : D0;
-  const uint32_t d1 = j2 ? D3 : j1 ? D2 : D1;
-  const int s1 = j3 ? L : j2 ? S3 : j1 ? S2 : S1;
-  const int s2 = j2 ? L : j1 ? S3 : S2;
-  c.A1 = (uint32_t)c.q0 + d0;
-  c.A2 = (uint32_t)c.q0 + d1;
-  c.B = s1 - c.q0;
-  c.two = s1 < hi;
-  c.clip = c.q0 < 0 || c.q0 + 16 > L;
-  c.slow = q < hi && (c.A1 > g.lim || (c.two && (s2 < hi || c.A2 > g.lim)));
-  return c;
-}
-// The chunk from its (at most two) loads: one mask per dword in the common
-// case, byte masks at the frame's ends, byte loads in the rare slow case.
-__device__ __forceinline__ u32x4 tx_build(const TxSegs &g, const TxCut &c, const u32x4 &xa, const u32x4 &xb,
-                                          __amdgpu_buffer_rsrc_t rs) {
-  u32x4 v{0, 0, 0, 0};
-  if (!c.clip && !c.slow) {
-    // bytes [0, B) from xa, [B, 16) from xb
-    const uint32_t b = (uint32_t)min(max(c.B, 0), 16);
-    const uint64_t lo = b >= 8u ? ~0ull : (1ull << (8u * b)) - 1u;
-    const uint64_t hm = b <= 8u ? 0ull : b >= 16u ? ~0ull : (1ull << (8u * (b - 8u))) - 1u;
-    v.x = (xa.x & (uint32_t)lo) | (xb.x & ~(uint32_t)lo);
-    v.y = (xa.y & (uint32_t)(lo >> 32)) | (xb.y & ~(uint32_t)(lo >> 32));
-    v.z = (xa.z & (uint32_t)hm) | (xb.z & ~(uint32_t)hm);
-    v.w = (xa.w & (uint32_t)(hm >> 32)) | (xb.w & ~(uint32_t)(hm >> 32));
-  } else if (!c.slow) {
-    const int lo = max(c.q0, 0) - c.q0, hi = min(c.q0 + 16, g.L) - c.q0;
-    merge_bytes(v, xa, lo, min(c.B, hi));
-    if (c.two) merge_bytes(v, xb, c.B, hi);
-  } else {
-    for (int q = max(c.q0, 0); q < min(c.q0 + 16, g.L); ++q) {
-      const uint32_t d = q >= g.S3 ? g.D3 : q >= g.S2 ? g.D2 : q >= g.S1 ? g.D1 : g.D0;
-      put_byte(v, q - c.q0, __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(q + (int)d), 0, 0));
-    }
-  }
-  return v;
-}
-
-// What ip_output decides for a frame from its IP header and m_pkthdr
-// (ip_output.c:649-672 with in_delayed_cksum, ip_output.c:958-983): which sums
-// to do, where the L4 one goes (at = hl + csum_data), and whether the datagram
-// is well-formed enough to be summed at all.
-struct TxPlan {
-  bool ok, do_ip, do_l4, udp;
-  uint32_t at;
-  int hend, lend;  // header / datagram length when ok, else 0
-};
-__device__ __forceinline__ TxPlan tx_plan(const TxDesc &t, uint32_t i, uint32_t len, const IpHdr &ih) {
-  TxPlan pl;
-  const uint32_t flen = len >= t.l3 ? len - t.l3 : 0u;
-  pl.ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl && ih.iplen <= flen;
-  const uint32_t fl =
-      t.cflags ? t.cflags[i] : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
-  pl.do_ip = pl.ok && (fl & MI_CSUM_IP);
-  pl.do_l4 = pl.ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
-  pl.udp = fl & MI_CSUM_UDP;
-  pl.at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? MI_CSUM_DATA_TCP : MI_CSUM_DATA_UDP);
-  pl.hend = pl.ok ? (int)ih.hl : 0;
-  pl.lend = pl.ok ? (int)ih.iplen : 0;
-  return pl;
-}
-__device__ __forceinline__ uint8_t tx_status(const TxPlan &pl, bool l4_store) {
-  return (uint8_t)((pl.ok ? 0u : MI_TX_NOSUM) | (pl.do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
-}
-
-// Generic gather of frame i by a G-lane group (long chains, an IP header split
-// over mbufs, sum fields far from the header): chunk-major over the whole
-// frame, every piece of every chunk gathered by walking the chain; chunks
-// stored as they are built, the sum fields patched once they have landed.
-// len, the chain [k0, k1) and ip_mlen come from the caller's chain walk.
-template <int G, int U>
-__device__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, uint32_t i,
-                                 int lane, uint32_t len, uint32_t k0, uint32_t k1, uint32_t ip_mlen) {
-  const uint32_t l3 = t.l3;
-  const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
-  const uint32_t h = D & 15u, c0 = D & ~15u;
-  const bool odd = (h + l3) & 1u;
-  IpHdr ih{};
-  TxPlan pl{};
-  uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
-  const uint32_t nch = (h + len + 15u) >> 4;
-  const uint32_t npass = (nch + G * U - 1) / (G * U);
-  for (uint32_t p = 0; p < npass; ++p) {
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int cs = (int)(16u * (p * (G * U) + u * G + lane)) - (int)h;
-      v[u] = u32x4{0, 0, 0, 0};
-      int pos = 0;
-      for (uint32_t k = k0; k < k1; ++k) {
-        const int l = max(t.seg_len[k], 0);
-        const int lo = max(pos - cs, 0), hi = min(min(pos + l, (int)len) - cs, 16);
-        if (hi > lo) {
-          const uint32_t a = (uint32_t)cs + ((uint32_t)t.seg_off[k] - (uint32_t)pos);
-          merge_bytes(v[u], shift_pair(ld_pair(rs, a), a), lo, hi);
-        }
-        pos += l;
-      }
-    }
-    if (p == 0) {
-      const u32x4 hv[1] = {v[0]};
-      ih = parse_ipv4<G, 1>(hv, h + l3);
-      pl = tx_plan(t, i, len, ih);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t ci = p * (G * U) + u * G + lane;
-      const int cs = (int)(16u * ci) - (int)h;
-      fold_chunk(v[u], cs - (int)l3, pl.lend, pl.hend, pl.hend > 20, acc_t, acc_h, acc_f);
-      if (ci < nch) store_chunk(rd, c0 + 16u * ci, v[u], -cs, (int)len - cs);
-    }
-  }
-  if (npass == 0) pl = TxPlan{};
-  const bool l4_store = pl.do_l4 && (uint64_t)pl.at + 2u <= ip_mlen;
-  uint32_t c_ip, c_l4;
-  tx_sums<G>(acc_t, acc_h, acc_f, pl.hend, ih, odd, pl.udp, c_ip, c_l4);
-  if (pl.do_ip || l4_store) {
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's chunk stores have landed
-    if (lane == 0) {
-      const uint32_t pip = l3 + 10u, pl4 = l3 + pl.at;
-      if (pl.do_ip) {
-        if (pip < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_ip, rd, D + pip, 0, 0);
-        if (pip + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_ip >> 8), rd, D + pip + 1u, 0, 0);
-      }
-      if (l4_store) {
-        if (pl4 < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_l4, rd, D + pl4, 0, 0);
-        if (pl4 + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_l4 >> 8), rd, D + pl4 + 1u, 0, 0);
-      }
-    }
-  }
-  if (lane == 0) t.status[i] = tx_status(pl, l4_store);
-}
-
-// U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
-// prefetch costs ~10 and a few spill to scratch): profiles/tx_copy_r02.jsonl,
-// socket frames 59-64 us per launch against 64-66 without the prefetch and
-// 69 with it at 3 waves per SIMD.
-template <int G, int U>
-__global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) {
-  static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
-  __shared__ uint32_t s_seg[kBlock / G][kTxSeg][2];
-  Desc ds{}, dd{};
-  ds.base = t.src;
-  ds.bytes = t.src_bytes;
-  dd.base = t.dst;
-  dd.bytes = t.dst_bytes;
-  const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
-  const int lane = threadIdx.x & (G - 1);
-  const uint32_t grp = (threadIdx.x & 255u) / G;
-  const uint32_t stride = gridDim.x * (kBlock / G);
-  // Descriptor prefetch: a frame's descriptors are a chain of two dependent
-  // loads (pkt_seg -> seg_len / seg_off) ahead of its first data load, so the
-  // NEXT frame's chain is walked while this frame's data is in flight -- the
-  // first level at the top of the iteration, the second level right after this
-  // frame's first data pass is issued (its wait then covers only the older
-  // descriptor loads; vmcnt is in order).  Lane j holds segment k0 + j.
-  uint32_t i = blockIdx.x * (kBlock / G) + threadIdx.x / G;
-  uint32_t len_c = 0, k0_c = 0, k1_c = 0;
-  int32_t sl_c = 0;
-  uint32_t so_c = 0;
-  if (i < t.n) {
-    len_c = t.pkt_len[i];
-    k0_c = t.pkt_seg[i];
-    k1_c = t.pkt_seg[i + 1];
-    if (k0_c + lane < k1_c) {
-      sl_c = t.seg_len[k0_c + lane];
-      so_c = (uint32_t)t.seg_off[k0_c + lane];
-    }
-  }
-  for (; i < t.n; i += stride) {
-    const uint32_t len = len_c;
-    const uint32_t k0 = k0_c, k1 = k1_c;
-    const int32_t sl0 = sl_c;
-    const uint32_t so0 = so_c;
-    const uint32_t in = i + stride;
-    uint32_t len_n = 0, k0_n = 0, k1_n = 0;
-    if (in < t.n) {
-      len_n = t.pkt_len[in];
-      k0_n = t.pkt_seg[in];
-      k1_n = t.pkt_seg[in + 1];
-    }
-    bool pre2 = false;
-    auto prefetch2 = [&]() {
-      if (pre2) return;
-      pre2 = true;
-      sl_c = 0;
-      so_c = 0;
-      if (in < t.n && k0_n + lane < k1_n) {
-        sl_c = t.seg_len[k0_n + lane];
-        so_c = (uint32_t)t.seg_off[k0_n + lane];
-      }
-      len_c = len_n;
-      k0_c = k0_n;
-      k1_c = k1_n;
-    };
-    const uint32_t l3 = t.l3;
-    const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
-    const uint32_t h = D & 15u, c0 = D & ~15u;
-    uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
-    // walk 1: bytes in the chain, the IP mbuf (segment holding frame byte l3)
-    // and its m_len from the IP header on, and the first kTxSeg nonempty
-    // segments (frame start, source offset - frame start) into LDS
-    uint32_t total = 0, ip_mlen = 0, m = 0;
-    for (uint32_t w = k0; w < k1 && !st; w += G) {
-      const uint32_t k = w + lane;
-      const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : t.seg_len[k], 0) : 0u;
-      const uint32_t inc = group_scan<G>(l);
-      const uint32_t a = total + inc - l, e = total + inc;
-      const uint32_t nz = l ? 1u : 0u;
-      const uint32_t zi = group_scan<G>(nz);
-      const uint32_t idx = m + zi - nz;
-      if (nz && idx < (uint32_t)kTxSeg) {
-        s_seg[grp][idx][0] = a;
-        s_seg[grp][idx][1] = (w == k0 ? so0 : (uint32_t)t.seg_off[k]) - a;
-      }
-      const bool isip = l && a <= l3 && l3 < e;
-      ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
-      total += group_lane<G>(inc, G - 1);
-      m += group_lane<G>(zi, G - 1);
-    }
-    if (!st && total < len) st = MI_TX_SHORT;
-    if (st) {
-      if (lane == 0) t.status[i] = (uint8_t)st;
-      prefetch2();
-      continue;
-    }
-    ip_mlen = group_lane<G>(ip_mlen, 0);
-    const bool odd = (h + l3) & 1u;  // parity of the IP header's destination address
-    IpHdr ih{};
-    bool ok = false, do_ip = false, do_l4 = false, udp = false, done = false;
-    uint32_t at = 0;
-    int hend = 0, lend = 0;
-    uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
-    auto decide1 = [&](const u32x4 &h0, uint32_t hoff) {
-      const u32x4 hv[1] = {h0};
-      ih = parse_ipv4<G, 1>(hv, hoff);
-      const TxPlan pl = tx_plan(t, i, len, ih);
-      ok = pl.ok;
-      do_ip = pl.do_ip;
-      do_l4 = pl.do_l4;
-      udp = pl.udp;
-      at = pl.at;
-      hend = pl.hend;
-      lend = pl.lend;
-    };
-    auto fold_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t p) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int rel = (int)(16u * (cfirst + p * (G * U) + u * G + lane)) - (int)(h + l3);
-        fold_chunk(v[u], rel, lend, hend, hend > 20, acc_t, acc_h, acc_f);
-      }
-    };
-    auto store_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t clast, uint32_t p, int pa, int pe,
-                         int u0 = 0) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (u < u0) continue;
-        const uint32_t ci = cfirst + p * (G * U) + u * G + lane;
-        const int cs = (int)(16u * ci) - (int)h;
-        if (ci < clast) store_chunk(rd, c0 + 16u * ci, v[u], pa - cs, pe - cs);
-      }
-    };
-    if (m <= (uint32_t)kTxSeg) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // segment e covers frame bytes [S[e], S[e+1]) (the last one: to len),
-      // frame byte q sits at source offset q + Dl[e]
-      static_assert(kTxSeg == 4, "segment registers S1..S3 / D0..D3");
-      auto seg_start = [&](uint32_t e) { return e < m ? min((int)s_seg[grp][e][0], (int)len) : (int)len; };
-      auto seg_delta = [&](uint32_t e) { return e < m ? s_seg[grp][e][1] : 0u; };
-      const uint32_t nch = (h + len + 15u) >> 4;
-      const uint32_t npass = (nch + G * U - 1) / (G * U);
-      // Chunk ci of the frame is gathered from at most two loads (tx_cut,
-      // tx_build above).
-      const int S1 = seg_start(1), S2 = seg_start(2), S3 = seg_start(3);
-      const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
-      const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
-      const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
-      u32x4 held{0, 0, 0, 0};
-      for (uint32_t p = 0; p < npass; ++p) {
-        u32x4 v[U];
-        u32x4 xa[U], xb[U];
-        TxCut cut[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
-          xa[u] = ld16_src(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
-          xb[u] = ld16_src(rs, c.two && !c.slow ? c.A2 : kOOB);
-          cut[u] = c;
-        }
-        if (p == 0) prefetch2();
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
-        if (p == 0) {
-          decide1(v[0], h + l3);
-          const uint32_t pip = l3 + 10u, pl4 = l3 + at;
-          const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-          const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
-          if ((uint64_t)need + h > 16ull * G) break;  // a sum field beyond the held chunks: generic path
-          done = true;
-          held = v[0];
-        }
-        fold_all(v, 0, p);
-        store_all(v, 0, nch, p, 0, (int)len, p == 0 ? 1 : 0);
-      }
-      if (npass == 0) {
-        ok = do_ip = do_l4 = false;
-        done = true;
-      }
-      if (done) {
-        const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-        uint32_t c_ip, c_l4;
-        tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
-        const uint32_t pip = l3 + 10u, pl4 = l3 + at;
-        const int b0 = (int)h - (int)(16u * lane);  // frame position -> byte of held
-        if (do_ip) {
-          if (pip < len) put_byte(held, (int)pip + b0, c_ip);
-          if (pip + 1u < len) put_byte(held, (int)pip + 1 + b0, c_ip >> 8);
-        }
-        if (l4_store) {
-          if (pl4 < len) put_byte(held, (int)pl4 + b0, c_l4);
-          if (pl4 + 1u < len) put_byte(held, (int)pl4 + 1 + b0, c_l4 >> 8);
-        }
-        const uint32_t ci = lane;
-        const int cs = (int)(16u * ci) - (int)h;
-        if (ci < nch) store_chunk(rd, c0 + 16u * ci, held, -cs, (int)len - cs);
-        if (lane == 0)
-          t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
-      }
-      __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
-    }
-    prefetch2();
-    if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
-  }
-}
+#include "tx_device.h"
 
 // Scalar drop-in path: one span in page-locked host memory (read over PCIe).
 // 8 waves: a pass reads 512 x 4 chunks (32 KiB), so a 64 KiB span costs two
@@ -2596,7 +1975,21 @@ Shape pick_tx_shape(uint32_t max_len) {
   return {8, 2};
 }
 
+// Which fused TX kernel: MI_CKSUM_TX_KERNEL = "pair" (k_tx_copy, a lane
+// group per frame, up to two loads per destination chunk) or "wave"
+// (k_tx_wave, a wave per frame, one load per slot).  Read per call so a test
+// can switch.
+int tx_kernel_kind() {
+  const char *e = getenv("MI_CKSUM_TX_KERNEL");
+  return e && !strcmp(e, "wave") ? 2 : 0;
+}
+
 int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
+  if (tx_kernel_kind() == 2) {
+    // one frame per wave: four per workgroup
+    hipLaunchKernelGGL((k_tx_wave<2>), dim3(grid_for(t.n, 64)), dim3(kBlock), 0, s, t);
+    return launched();
+  }
   const int grid = grid_for(t.n, sh.g);
 #define X(G_, U_)                                                                  \
   if (sh.g == G_ && sh.u == U_) {                                                  \

@@ -197,7 +197,8 @@ def _frame_byte(c, i, q):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(TX_BIN), reason="tx_test not built (needs /root/reference at build time)")
-def test_tx_offload_matches_reference_software_route(tmp_path):
+@pytest.mark.parametrize("kernel", ["pair", "wave"])
+def test_tx_offload_matches_reference_software_route(tmp_path, kernel):
     """VERDICT r3 "do this" 1: every tests/tx_cases.py case goes out twice
     through real struct mbufs of the reference's definition -- if_hwassist = 0
     (ip_output.c:649-672 + in_delayed_cksum :958-983 with the reference's own
@@ -211,10 +212,11 @@ def test_tx_offload_matches_reference_software_route(tmp_path):
     for name, c in _tx_cases():
         p = tmp_path / f"{name}.bin"
         _tx_case_file(p, c)
-        r = subprocess.run([TX_BIN, str(p)], capture_output=True, text=True, timeout=120)
+        r = subprocess.run([TX_BIN, str(p)], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, MI_CKSUM_TX_KERNEL=kernel))
         assert r.stdout.strip(), r.stderr
         res = json.loads(r.stdout)
-        print(name, json.dumps(res))
+        print(kernel, name, json.dumps(res))
         assert r.returncode == 0, (name, res)
         for k in ("byte_mismatch_zero_copy", "byte_mismatch_staged", "status_mismatch_zero_copy",
                   "status_mismatch_staged"):
