@@ -2542,6 +2542,24 @@ struct AqlOne {
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
 
+// Drop-in latency breakdown (diagnostics, mi__dropin_trace): with tracing on,
+// the thread's drop-in dispatches carry the completion signal and queue
+// profiling, and each call records, in the HSA system timestamp domain: fold
+// entry, the doorbell written, the kernel's start and end (dispatch
+// timestamps converted to the system domain), the result word seen by the
+// host.
+struct DropinTrace {
+  bool on = false;
+  uint64_t t_entry = 0, t_doorbell = 0, t_seen = 0, g_start = 0, g_end = 0;
+  double us_per_tick = 0.0;
+};
+thread_local DropinTrace t_dtrace;
+uint64_t sys_ts() {
+  uint64_t t = 0;
+  (void)hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP, &t);
+  return t;
+}
+
 // Reserve the next packet slot of the thread's queue (deadline-bounded).
 int aql_one_slot(AqlOne &o, uint64_t *idx, void **slot) {
   *idx = hsa_queue_add_write_index_screlease(o.q, 1);
@@ -2659,6 +2677,7 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
     if (rc) return rc;
     o.err = new std::atomic<int>(0);
     if ((rc = aql_queue_create(o.dev->agent, 64, o.err, &o.q))) return rc;
+    if (t_dtrace.on) (void)hsa_amd_profiling_set_profiler_enabled(o.q, 1);
     if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
       aql_one_release(o);
       return set_err(-EIO, "AQL engine: hsa_signal_create failed");
@@ -2685,8 +2704,9 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   if (rc) return rc;
   hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)p;
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
-  if (wait) hsa_signal_store_relaxed(o.sig, 1);
-  slot->completion_signal = wait ? o.sig : hsa_signal_t{0};
+  const bool sig = wait || t_dtrace.on;  // tracing: the dispatch timestamps need the signal
+  if (sig) hsa_signal_store_relaxed(o.sig, 1);
+  slot->completion_signal = sig ? o.sig : hsa_signal_t{0};
   // system-scope fences both ways: the kernels read host memory the host
   // rewrites every call (burst, staging, descriptors) and write host memory
   const uint32_t sc = HSA_FENCE_SCOPE_SYSTEM;
@@ -2695,6 +2715,7 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
                       ((uint32_t)t.setup << 16);
   __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
   hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
+  if (t_dtrace.on) t_dtrace.t_doorbell = sys_ts();
   if (!wait) {
     o.unretired = true;
     return 0;
@@ -3914,6 +3935,7 @@ uint8_t *mi__scalar_staging(size_t need) {
 // time-sliced) only makes the call slower.
 int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32_t src,
                     uint32_t dst, uint8_t proto, uint32_t plen, uint16_t *out) {
+  if (t_dtrace.on) t_dtrace.t_entry = sys_ts();
   int rc = ensure_ctx();
   if (rc) return rc;
   ThreadCtx &c = t_ctx;
@@ -3983,6 +4005,46 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     }
   }
   *out = (uint16_t)(v & 0xffffu);
+  if (t_dtrace.on && used_aql) {
+    t_dtrace.t_seen = sys_ts();
+    // retire the dispatch (its signal) and read its timestamps
+    if ((rc = aql_one_wait(t_aql1))) return rc;
+    hsa_amd_profiling_dispatch_time_t dt{};
+    if (hsa_amd_profiling_get_dispatch_time(t_aql1.dev->agent, t_aql1.sig, &dt) == HSA_STATUS_SUCCESS) {
+      (void)hsa_amd_profiling_convert_tick_to_system_domain(t_aql1.dev->agent, dt.start, &t_dtrace.g_start);
+      (void)hsa_amd_profiling_convert_tick_to_system_domain(t_aql1.dev->agent, dt.end, &t_dtrace.g_end);
+    }
+  }
+  return 0;
+}
+
+// Diagnostics (not in the public header): drop-in latency breakdown.
+// mi__dropin_trace(1) switches the calling thread's drop-ins to traced
+// dispatches (completion signal + queue profiling); mi__dropin_trace_read
+// returns, for the last call, in us from fold entry: [doorbell written,
+// kernel start, kernel end, result seen by the host].
+int mi__dropin_trace(int on) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (on && !t_dtrace.us_per_tick) {
+    uint64_t f = 0;
+    if (hsa_system_get_info(HSA_SYSTEM_INFO_TIMESTAMP_FREQUENCY, &f) != HSA_STATUS_SUCCESS || !f)
+      return set_err(-EIO, "no system timestamp frequency");
+    t_dtrace.us_per_tick = 1e6 / (double)f;
+  }
+  // the queue must have profiling on before the traced dispatches
+  if (on && t_aql1.q) (void)hsa_amd_profiling_set_profiler_enabled(t_aql1.q, 1);
+  t_dtrace.on = on != 0;
+  return 0;
+}
+int mi__dropin_trace_read(double *out, int n) {
+  if (!out || n < 4) return set_err(-EINVAL, "need 4 doubles");
+  const DropinTrace &t = t_dtrace;
+  auto us = [&](uint64_t x) { return x ? ((double)x - (double)t.t_entry) * t.us_per_tick : -1.0; };
+  out[0] = us(t.t_doorbell);
+  out[1] = us(t.g_start);
+  out[2] = us(t.g_end);
+  out[3] = us(t.t_seen);
   return 0;
 }
 

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Where the ~8 us of a (b1) drop-in call goes (VERDICT r3 "do this" 6).
+
+With mi__dropin_trace(1) the calling thread's drop-in dispatches carry a
+completion signal and queue profiling, and every call records, in the HSA
+system timestamp domain, from the fold's entry: the doorbell written, the
+kernel's start and end (AQL dispatch timestamps converted to the system
+domain), and the moment the host sees the result word.  Median over N calls of
+each (b1) function on real mbuf chains, next to the untraced per-call time
+(the traced dispatch's signal costs a little, so the phases are shares).
+
+    python tools/dropin_breakdown.py [--calls 400] > dropin_breakdown.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (one HIP runtime per process: torch's)
+
+import libunsod_amd as mi  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--calls", type=int, default=400)
+    a = ap.parse_args()
+    lib = mi.load()
+    lib.mi__dropin_trace.argtypes = [C.c_int]
+    lib.mi__dropin_trace_read.argtypes = [C.POINTER(C.c_double), C.c_int]
+    pat = bytes(i & 0xFF for i in range(65536))
+    m64 = mi.MbufChain([pat])
+    ip_hdr = bytes.fromhex("450005dc0000400040060000c0a80101c0a80102")
+    m1500 = mi.MbufChain([ip_hdr + pat[:1480]])
+    hraw = np.zeros(256, np.uint8)
+    hoff = 64 + ((2 - (hraw.ctypes.data + 64)) % 64)
+    hraw[hoff:hoff + 20] = np.frombuffer(ip_hdr, np.uint8)
+    haddr = hraw.ctypes.data + hoff
+    src, dst = 0x0101A8C0, 0x0201A8C0
+    cases = {
+        "in_cksum_hdr_20B": (lib.in_cksum_hdr, (C.c_void_p(haddr),)),
+        "in_cksum_pseudo_header_1480B": (lib.in_cksum_pseudo_header, (C.c_void_p(m1500.ptr), 1480, 20, src, dst, 6)),
+        "in_cksum_skip_65536B": (lib.in_cksum_skip, (C.c_void_p(m64.ptr), 65536, 0)),
+    }
+    out = (C.c_double * 4)()
+    for name, (fn, args) in cases.items():
+        fn(*args)
+        plain = []
+        for _ in range(a.calls):
+            t0 = time.perf_counter()
+            fn(*args)
+            plain.append(time.perf_counter() - t0)
+        assert lib.mi__dropin_trace(1) == 0
+        fn(*args)
+        rows, tot = [], []
+        for _ in range(a.calls):
+            t0 = time.perf_counter()
+            fn(*args)
+            tot.append(time.perf_counter() - t0)
+            lib.mi__dropin_trace_read(out, 4)
+            rows.append(list(out))
+        assert lib.mi__dropin_trace(0) == 0
+        r = np.array(rows)
+        med = lambda x: round(float(np.median(x)), 3)  # noqa: E731
+        print(json.dumps(dict(
+            call=name, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6), traced_call_us=med(np.array(tot) * 1e6),
+            entry_to_doorbell_us=med(r[:, 0]),
+            doorbell_to_kernel_start_us=med(r[:, 1] - r[:, 0]),
+            kernel_us=med(r[:, 2] - r[:, 1]),
+            kernel_start_to_result_seen_us=med(r[:, 3] - r[:, 1]),
+            entry_to_result_seen_us=med(r[:, 3]),
+            note="system-domain timestamps from the fold's entry (after the mbuf walk and staging copy); "
+                 "call_us = the whole ctypes call measured in Python")), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,4 +19,6 @@ timeout -k 10 500 python -u tools/ab.py --config pareto --rounds 3 --steps 200 w
 cut -c1-160 $O/ab_pareto_waves.jsonl
 timeout -k 10 300 python -u tools/grid_iso.py --config 1500 --caps 1024,1280,2048,2560 > $O/grid_iso.jsonl 2> $O/grid_iso.err || exit 1
 cut -c1-250 $O/grid_iso.jsonl
+timeout -k 10 120 python -u tools/dropin_breakdown.py --calls 400 > $O/dropin_breakdown.jsonl 2> $O/dropin.err || exit 1
+cut -c1-300 $O/dropin_breakdown.jsonl
 echo done
