@@ -130,7 +130,21 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
   Desc d = a.e[0].d;
   uint16_t *ipo = a.e[0].ip, *l4o = a.e[0].l4;
   uint8_t *sto = a.e[0].st;
-  for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
+  // Units come from a static grid stride, or (a.ctr) from a device counter:
+  // each wave takes its next unit when it starts on the current one (the
+  // atomic's round trip hides under the unit's loads), so a wave that runs
+  // faster takes more units and the launch ends within about one unit of
+  // its last wave instead of waiting for the slowest wave's fixed share.
+  // The counter pair is reset by the last wave to finish, for the next
+  // launch on it.
+  const bool dyn = a.ctr != nullptr;
+  const bool lead = (threadIdx.x & 63u) == 0;
+  uint32_t take = 0;
+  if (dyn && lead) take = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t u = dyn ? __builtin_amdgcn_readfirstlane(take) : blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  for (; u < a.units;) {
+    uint32_t un = u + nwaves;
+    if (dyn && lead) take = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (u >= next) {
       do {
         ++j;
@@ -144,17 +158,26 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
     }
     const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
     const uint32_t i = (u - u0) * gpw + gid;
-    if (i >= d.n) continue;  // the batch's last unit: whole groups drop out
-    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
-    u32x4 v[U];
-    issue_first<G, U>(r, off, flen, lane, v);
-    IpHdr ih;
-    bool hdr_ok, l4_ok;
-    uint32_t sum_h, sum_l;
-    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
-    if (lane == 0)
-      verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
-                  ipo, l4o, sto, a.bad, d);
+    if (i < d.n) {  // (the batch's last unit: whole groups drop out)
+      const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+      u32x4 v[U];
+      issue_first<G, U>(r, off, flen, lane, v);
+      IpHdr ih;
+      bool hdr_ok, l4_ok;
+      uint32_t sum_h, sum_l;
+      ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+      if (lane == 0)
+        verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
+                    ipo, l4o, sto, a.bad, d);
+    }
+    if (dyn) un = __builtin_amdgcn_readfirstlane(take);
+    u = un;
+  }
+  if (dyn && lead &&
+      __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwaves - 1u) {
+    // every wave has taken its last (out-of-range) unit: reset for the next launch
+    __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1464,6 +1487,11 @@ struct ThreadCtx {
   // zero-copy host path: descriptors / outputs in mapped host memory (grown on demand)
   uint8_t *zhost = nullptr, *zhost_dev = nullptr;
   size_t zhost_cap = 0;
+  // dynamic unit counters of multi-batch launches (kMultiCtr pairs, 64 B
+  // apart, zeroed; each launch takes the next pair and its last wave resets it)
+  static constexpr uint32_t kMultiCtr = 64;
+  uint32_t *mctr = nullptr;
+  uint32_t mctr_next = 0;
   // staged TX host path: source blob, slot region, descriptors (device)
   uint8_t *tx_src = nullptr, *tx_dst = nullptr, *tx_desc = nullptr;
   size_t tx_src_cap = 0, tx_dst_cap = 0, tx_desc_cap = 0;
@@ -1526,6 +1554,7 @@ void ctx_release(ThreadCtx &c, int back) {
     dfree(c.dflag[k]);
   }
   dfree(c.dbad);
+  dfree(c.mctr);
   hfree(c.zhost);
   dfree(c.tx_src);
   dfree(c.tx_dst);
@@ -2886,6 +2915,19 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
   a.nb = nb;
   a.units = units;
   if (!units) return 0;
+  // dynamic unit scheduling (MI_CKSUM_MULTI_DYN=1; else the static grid
+  // stride).  A counter pair is reused kMultiCtr launches later: at most that
+  // many multi-batch launches of one thread may be in flight at once.
+  const char *dyn_env = getenv("MI_CKSUM_MULTI_DYN");  // per call, so a test can switch
+  const bool dyn = dyn_env && dyn_env[0] == '1';
+  if (dyn) {
+    ThreadCtx &c = t_ctx;
+    if (!c.mctr) {
+      HIP_TRY(hipMalloc((void **)&c.mctr, 64u * ThreadCtx::kMultiCtr));
+      HIP_TRY(hipMemset(c.mctr, 0, 64u * ThreadCtx::kMultiCtr));
+    }
+    a.ctr = c.mctr + 16u * (c.mctr_next++ % ThreadCtx::kMultiCtr);
+  }
   // Grid: as many blocks as can be resident at once (occupancy x CUs), so
   // every wave streams its units from the start to the end of the launch.  A
   // larger grid (round 1: 2048 blocks of which ~1280 fit) runs in two rounds:
