@@ -10,9 +10,12 @@
  *  (b1) drop-in scalar entry points with the reference's exact names and
  *       signatures -- they replace the MACHINE_SRCS object in_cksum.o inside
  *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  Each call
- *       gathers the mbuf chain into a per-thread pinned staging buffer and runs
- *       one HIP launch, so a call costs a launch + sync (~10-20 us); the
- *       bandwidth path is (b2).
+ *       gathers the mbuf chain into a per-thread pinned staging buffer and
+ *       writes one AQL dispatch packet into a per-thread HSA queue of the
+ *       library's, then spins on a pinned result word: ~8-11 us per call on the
+ *       MI355X host.  This level is the compatibility path (the
+ *       reference's call sites unchanged); per-packet RX/TX throughput comes
+ *       from (b2) at the burst / inject-ring batch points.
  *
  *  (b2) batch offload: a batch of packets that already sits in device memory
  *       (the RX burst / TX inject-ring batch points, uinet_if_dpdk.c:854-879 and

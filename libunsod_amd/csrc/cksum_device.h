@@ -655,7 +655,6 @@ struct MultiArgs {
   uint32_t nb, units;
   uint32_t *bad;
   MultiEnt e[kMaxMulti];
-  uint32_t *ctr;  // dynamic unit scheduling: [next unit, waves done], or NULL (static)
 };
 
 }  // namespace

@@ -130,21 +130,7 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
   Desc d = a.e[0].d;
   uint16_t *ipo = a.e[0].ip, *l4o = a.e[0].l4;
   uint8_t *sto = a.e[0].st;
-  // Units come from a static grid stride, or (a.ctr) from a device counter:
-  // each wave takes its next unit when it starts on the current one (the
-  // atomic's round trip hides under the unit's loads), so a wave that runs
-  // faster takes more units and the launch ends within about one unit of
-  // its last wave instead of waiting for the slowest wave's fixed share.
-  // The counter pair is reset by the last wave to finish, for the next
-  // launch on it.
-  const bool dyn = a.ctr != nullptr;
-  const bool lead = (threadIdx.x & 63u) == 0;
-  uint32_t take = 0;
-  if (dyn && lead) take = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  uint32_t u = dyn ? __builtin_amdgcn_readfirstlane(take) : blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  for (; u < a.units;) {
-    uint32_t un = u + nwaves;
-    if (dyn && lead) take = __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
     if (u >= next) {
       do {
         ++j;
@@ -158,26 +144,17 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
     }
     const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
     const uint32_t i = (u - u0) * gpw + gid;
-    if (i < d.n) {  // (the batch's last unit: whole groups drop out)
-      const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
-      u32x4 v[U];
-      issue_first<G, U>(r, off, flen, lane, v);
-      IpHdr ih;
-      bool hdr_ok, l4_ok;
-      uint32_t sum_h, sum_l;
-      ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
-      if (lane == 0)
-        verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
-                    ipo, l4o, sto, a.bad, d);
-    }
-    if (dyn) un = __builtin_amdgcn_readfirstlane(take);
-    u = un;
-  }
-  if (dyn && lead &&
-      __hip_atomic_fetch_add(a.ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nwaves - 1u) {
-    // every wave has taken its last (out-of-range) unit: reset for the next launch
-    __hip_atomic_store(a.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i >= d.n) continue;  // the batch's last unit: whole groups drop out
+    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    u32x4 v[U];
+    issue_first<G, U>(r, off, flen, lane, v);
+    IpHdr ih;
+    bool hdr_ok, l4_ok;
+    uint32_t sum_h, sum_l;
+    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    if (lane == 0)
+      verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
+                  ipo, l4o, sto, a.bad, d);
   }
 }
 
@@ -1400,11 +1377,18 @@ extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint1
                                                                    uint32_t *bad) {
   slot64_body(d, ip, l4, st, bad);
 }
-// (the same kernel serves the HIP launch and the AQL one-shot dispatch, hence extern "C")
-extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
-                                                          uint32_t len, uint32_t abs_lanes, int pseudo,
-                                                          uint32_t src, uint32_t dst, uint32_t proto,
-                                                          uint32_t plen, uint32_t tag, uint32_t *out) {
+namespace {
+// The 100 MHz constant clock (the clock of the queues' dispatch timestamps).
+__device__ __forceinline__ uint64_t rt_clock() {
+  uint64_t t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+// One span in page-locked host memory folded by the kScalarThreads lanes of
+// a workgroup; lane 0 gets in_cksum_skip's / in_cksum_pseudo_header's value.
+__device__ __forceinline__ uint32_t scalar_span(const uint8_t *base, uint32_t bytes, uint32_t off, uint32_t len,
+                                                uint32_t abs_lanes, uint32_t pseudo, uint32_t src, uint32_t dst,
+                                                uint32_t proto, uint32_t plen, uint32_t *part) {
   Desc d{};
   d.len_hi = ~0u;
   d.base = base; d.bytes = bytes; d.n = 1; d.first_off = off; d.fixed_len = len;
@@ -1425,10 +1409,10 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
     }
     acc = fold16(acc);
   }
-  __shared__ uint32_t part[kScalarThreads / 64];
   acc = group_sum<64>(acc);
   if ((lane & 63) == 0) part[lane >> 6] = acc;
   __syncthreads();
+  uint32_t res = 0;
   if (lane == 0) {
     uint64_t sum = 0;
 #pragma unroll
@@ -1436,8 +1420,84 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
     sum = fold16_64(sum);
     if (!abs_lanes && (((uintptr_t)base + off) & 1u)) sum = swap16((uint32_t)sum);
     if (pseudo) sum += (uint64_t)src + dst + (proto << 8) + swap16(plen & 0xffffu);
-    const uint32_t res = ~fold16_64(sum) & 0xffffu;
-    __hip_atomic_store(out, (tag << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    res = ~fold16_64(sum) & 0xffffu;
+  }
+  return res;
+}
+}  // namespace
+
+// (the same kernel serves the HIP launch and the AQL one-shot dispatch, hence
+// extern "C").  tag bit 31: also store the kernel's start and end on the
+// 100 MHz clock at out[2..5] (the drop-in latency breakdown).
+extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const uint8_t *base, uint32_t bytes, uint32_t off,
+                                                          uint32_t len, uint32_t abs_lanes, int pseudo,
+                                                          uint32_t src, uint32_t dst, uint32_t proto,
+                                                          uint32_t plen, uint32_t tag, uint32_t *out) {
+  const uint64_t t0 = rt_clock();
+  __shared__ uint32_t part[kScalarThreads / 64];
+  const uint32_t res = scalar_span(base, bytes, off, len, abs_lanes, (uint32_t)pseudo, src, dst, proto, plen, part);
+  if (threadIdx.x == 0) {
+    if (tag >> 31) {
+      const uint64_t t1 = rt_clock();
+      __hip_atomic_store((uint64_t *)(out + 2), t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store((uint64_t *)(out + 4), t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(out, ((tag & 0xffffu) << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The drop-in service (MI_CKSUM_DROPIN_SERVICE): one workgroup that stays
+// resident while its thread keeps calling drop-ins, so a call costs no queue
+// dispatch -- the host writes the request into a mailbox in coherent
+// page-locked memory (box[1..10]: cmd, off, len, abs_lanes, pseudo, src, dst,
+// proto, plen, trace; then box[0], the request's sequence word, with release
+// order),
+// lane 0 polls box[0] with system-scope loads, the workgroup folds the span and
+// stores the tagged result as mi_aql_scalar does.  Exit conditions every wave
+// reaches: a stop request (cmd 1), or no new request for idle_ticks of the
+// 100 MHz clock -- the host sees the dispatch retire (its completion signal)
+// and launches a new one when the next call comes.  With trace set, out[2..5]
+// get the clock at the moment the request was seen and at the result store.
+extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
+                                                                             const uint32_t *box, uint32_t *out,
+                                                                             uint32_t seq0, uint32_t idle_ticks) {
+  __shared__ uint32_t part[kScalarThreads / 64];
+  __shared__ uint32_t req[11];
+  uint32_t last = seq0;
+  uint64_t t_last = rt_clock();
+  for (;;) {
+    if (threadIdx.x == 0) {
+      uint32_t sq;
+      for (;;) {
+        sq = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (sq != last || rt_clock() - t_last > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (sq != last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#pragma unroll
+        for (int k = 1; k < 11; ++k) req[k] = __hip_atomic_load(box + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      req[0] = sq;
+    }
+    __syncthreads();
+    const uint32_t sq = req[0];
+    if (sq == last || req[1] != 0u) break;  // idle, or a stop request
+    const uint64_t t_seen = rt_clock();
+    // every wave: the staging bytes are ordinary page-locked memory the host
+    // rewrote since the last request -- no cached copy of them may be used
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t res = scalar_span(base, bytes, req[2], req[3], req[4], req[5], req[6], req[7], req[8], req[9], part);
+    if (threadIdx.x == 0) {
+      if (req[10]) {
+        __hip_atomic_store((uint64_t *)(out + 2), t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store((uint64_t *)(out + 4), rt_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __hip_atomic_store(out, ((sq & 0xffffu) << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    last = sq;
+    t_last = rt_clock();
+    __syncthreads();  // req[] and part[] are rewritten by the next request
   }
 }
 
@@ -1487,11 +1547,6 @@ struct ThreadCtx {
   // zero-copy host path: descriptors / outputs in mapped host memory (grown on demand)
   uint8_t *zhost = nullptr, *zhost_dev = nullptr;
   size_t zhost_cap = 0;
-  // dynamic unit counters of multi-batch launches (kMultiCtr pairs, 64 B
-  // apart, zeroed; each launch takes the next pair and its last wave resets it)
-  static constexpr uint32_t kMultiCtr = 64;
-  uint32_t *mctr = nullptr;
-  uint32_t mctr_next = 0;
   // staged TX host path: source blob, slot region, descriptors (device)
   uint8_t *tx_src = nullptr, *tx_dst = nullptr, *tx_desc = nullptr;
   size_t tx_src_cap = 0, tx_dst_cap = 0, tx_desc_cap = 0;
@@ -1554,7 +1609,6 @@ void ctx_release(ThreadCtx &c, int back) {
     dfree(c.dflag[k]);
   }
   dfree(c.dbad);
-  dfree(c.mctr);
   hfree(c.zhost);
   dfree(c.tx_src);
   dfree(c.tx_dst);
@@ -1778,14 +1832,16 @@ int run_dma_code() {
 }
 
 // Waves per workgroup of the flat-run verify (MI_CKSUM_RUN_WAVES = 1, 2 or 4;
-// mi__set_run_waves for tests).
+// mi__set_run_waves for tests).  2 by default: on the 2^22 Pareto batch 2-wave
+// workgroups ran 196.8-197.5 us against 203.1-203.5 (4 waves) and 201.8-202.5
+// (1 wave), same box, interleaved (profiles/r04/ab_pareto_waves_r04.jsonl).
 std::atomic<int> g_run_waves{0};
 int run_waves() {
   int w = g_run_waves.load(std::memory_order_relaxed);
   if (!w) {
     const char *e = getenv("MI_CKSUM_RUN_WAVES");
     const int v = e ? atoi(e) : 0;
-    w = v == 1 || v == 2 ? v : 4;
+    w = v == 1 || v == 4 ? v : 2;
     g_run_waves.store(w, std::memory_order_relaxed);
   }
   return w;
@@ -2050,7 +2106,7 @@ enum AqlKernelId {
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
-  kAqlSlot64, kAqlScalar, kAqlKernels
+  kAqlSlot64, kAqlScalar, kAqlSvc, kAqlKernels
 };
 const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
@@ -2060,7 +2116,7 @@ const char *const kAqlNames[kAqlKernels] = {
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    "mi_aql_slot64", "mi_aql_scalar"};
+    "mi_aql_slot64", "mi_aql_scalar", "mi_aql_dropin_svc"};
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
@@ -2070,7 +2126,7 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar};
+    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar, (const void *)mi_aql_dropin_svc};
 
 // The kernels' explicit arguments, laid out as the compiler lays out the
 // kernel-argument segment (each parameter at its natural alignment).  The
@@ -2567,6 +2623,10 @@ struct AqlOne {
   // report into it after the thread has gone (it is leaked with the queue)
   std::atomic<int> *err = nullptr;
   int error() const { return err ? err->load() : 0; }
+  // the drop-in service (mi_aql_dropin_svc) running on this queue, and its
+  // mailbox (coherent page-locked host memory, ThreadCtx::sout + 16 words)
+  bool svc_live = false;
+  uint32_t *svc_box = nullptr;
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
@@ -2609,8 +2669,24 @@ int aql_one_wait(AqlOne &o) {
   }
   return 0;
 }
+// Stop the thread's drop-in service and wait for its dispatch to retire: a
+// stop request (cmd 1) under a sequence word no tag can equal (bit 16 set).
+int svc_stop(AqlOne &o) {
+  if (!o.svc_live) return 0;
+  volatile uint32_t *bx = o.svc_box;
+  bx[1] = 1u;
+  __atomic_store_n(&o.svc_box[0], (bx[0] + 0x10000u) | 0x10000u, __ATOMIC_RELEASE);
+  int rc = aql_one_wait(o);
+  if (rc) return rc;
+  o.svc_live = false;
+  o.unretired = false;  // its barrier bit ordered it after every earlier packet
+  return 0;
+}
+
 // Every packet of the thread's queue retired (a barrier-AND packet behind them).
 int aql_one_quiesce(AqlOne &o) {
+  int src = svc_stop(o);
+  if (src) return src;
   if (!o.unretired) return 0;
   uint64_t idx;
   void *p;
@@ -2662,6 +2738,8 @@ bool aql_one_release(AqlOne &o) {
   o.next = 0;
   o.unretired = false;
   o.err = nullptr;
+  o.svc_live = false;
+  o.svc_box = nullptr;
   return leaked;
 }
 
@@ -2695,18 +2773,23 @@ void thread_exit_register() {
 
 // nargs explicit argument bytes at args (laid out like the kernel's
 // parameters); wait: spin on the completion signal (else the kernel signals
-// the caller itself, e.g. through a pinned host word)
-// sys: acquire / release at system scope (host-memory data the kernel reads
-// through caches or writes with plain stores); else agent scope
-int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait) {
+// the caller itself, e.g. through a pinned host word); signal: give the
+// dispatch the completion signal without waiting (the drop-in service, whose
+// retirement the caller watches).  A running drop-in service is stopped first:
+// the packet behind it would wait for it (barrier bit).
+int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait,
+                   bool signal = false) {
   AqlOne &o = t_aql1;
+  if (o.svc_live) {
+    int rc = svc_stop(o);
+    if (rc) return rc;
+  }
   if (o.device != t_ctx.device) {
     if (aql_one_release(o)) return set_err(-EIO, "AQL engine: the thread's previous queue never retired");
     int rc = aql_device(t_ctx.device, &o.dev);
     if (rc) return rc;
     o.err = new std::atomic<int>(0);
     if ((rc = aql_queue_create(o.dev->agent, 64, o.err, &o.q))) return rc;
-    if (t_dtrace.on) (void)hsa_amd_profiling_set_profiler_enabled(o.q, 1);
     if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
       aql_one_release(o);
       return set_err(-EIO, "AQL engine: hsa_signal_create failed");
@@ -2733,7 +2816,7 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   if (rc) return rc;
   hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)p;
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
-  const bool sig = wait || t_dtrace.on;  // tracing: the dispatch timestamps need the signal
+  const bool sig = wait || signal;
   if (sig) hsa_signal_store_relaxed(o.sig, 1);
   slot->completion_signal = sig ? o.sig : hsa_signal_t{0};
   // system-scope fences both ways: the kernels read host memory the host
@@ -2915,19 +2998,6 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
   a.nb = nb;
   a.units = units;
   if (!units) return 0;
-  // dynamic unit scheduling (MI_CKSUM_MULTI_DYN=1; else the static grid
-  // stride).  A counter pair is reused kMultiCtr launches later: at most that
-  // many multi-batch launches of one thread may be in flight at once.
-  const char *dyn_env = getenv("MI_CKSUM_MULTI_DYN");  // per call, so a test can switch
-  const bool dyn = dyn_env && dyn_env[0] == '1';
-  if (dyn) {
-    ThreadCtx &c = t_ctx;
-    if (!c.mctr) {
-      HIP_TRY(hipMalloc((void **)&c.mctr, 64u * ThreadCtx::kMultiCtr));
-      HIP_TRY(hipMemset(c.mctr, 0, 64u * ThreadCtx::kMultiCtr));
-    }
-    a.ctr = c.mctr + 16u * (c.mctr_next++ % ThreadCtx::kMultiCtr);
-  }
   // Grid: as many blocks as can be resident at once (occupancy x CUs), so
   // every wave streams its units from the start to the end of the launch.  A
   // larger grid (round 1: 2048 blocks of which ~1280 fit) runs in two rounds:
@@ -3969,12 +4039,37 @@ uint8_t *mi__scalar_staging(size_t need) {
   return c.stage;
 }
 
-// One dispatch; the kernel stores (tag << 16) | sum into the pinned slot with
-// a system-scope store and the host spins on the slot (a few us sooner than
-// the completion signal).  The spin also watches the dispatch itself: a kernel
-// that retires without storing the word, a queue error or a 10 s wall-clock
-// deadline end the call with an error, never a hang; a slow GPU (busy,
-// time-sliced) only makes the call slower.
+// The drop-in service switch (MI_CKSUM_DROPIN_SERVICE=1, mi__set_dropin_service)
+// and its idle exit (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).
+std::atomic<int> g_dropin_svc{-1};
+bool dropin_svc_on() {
+  int v = g_dropin_svc.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE");
+    v = e && e[0] == '1' ? 1 : 0;
+    g_dropin_svc.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+uint32_t dropin_svc_idle_ticks() {
+  static const uint32_t t = [] {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_IDLE_US");
+    const long us = e ? atol(e) : 0;
+    return (uint32_t)((us > 0 && us < 10000000 ? us : 1000) * 100);  // the 100 MHz clock
+  }();
+  return t;
+}
+
+// One (b1) fold.  The kernel stores (tag << 16) | sum into the pinned slot
+// with a system-scope store and the host spins on the slot (a few us sooner
+// than a completion signal).  Either one dispatch per call (mi_aql_scalar: an
+// AQL packet into the thread's queue, or with MI_CKSUM_HOST_AQL=0 a HIP
+// launch), or, with the drop-in service on, a request into the mailbox of the
+// thread's resident mi_aql_dropin_svc workgroup (launched by the first call and
+// again whenever it has retired on its idle exit).  The spin also watches the
+// work itself: a kernel that retires without storing the word, a queue error
+// or a 10 s wall-clock deadline end the call with an error, never a hang; a
+// slow GPU (busy, time-sliced) only makes the call slower.
 int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32_t src,
                     uint32_t dst, uint8_t proto, uint32_t plen, uint16_t *out) {
   if (t_dtrace.on) t_dtrace.t_entry = sys_ts();
@@ -3985,15 +4080,15 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     return set_err(-EINVAL, "scalar staging overrun");
   if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
   if (!c.sout) {
-    HIP_TRY(hipHostMalloc((void **)&c.sout, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    // words 0..5: the result and the trace stamps; 16..26: the service mailbox
+    HIP_TRY(hipHostMalloc((void **)&c.sout, 128, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
-    memset(c.sout, 0, 64);
+    memset(c.sout, 0, 128);
   }
   c.stag = (c.stag + 1) & 0xffffu;
   const uint32_t tag = c.stag;
-  // One dispatch packet into the thread's HSA queue (MI_CKSUM_HOST_AQL=0: a
-  // HIP launch); either way the kernel stores the tagged result straight into
-  // the pinned word spun on below.
+  const bool trace = t_dtrace.on;
+  if (trace) memset(c.sout + 2, 0, 16);
   struct ScalarArgs {  // mi_aql_scalar's parameters, in order
     const uint8_t *base;
     uint32_t bytes, off, len, abs_lanes;
@@ -4002,25 +4097,62 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     uint32_t *out;
   };
   static_assert(sizeof(ScalarArgs) == 56, "kernel-argument layout of mi_aql_scalar");
+  struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
+    const uint8_t *base;
+    uint32_t bytes, pad_;
+    const uint32_t *box;
+    uint32_t *out;
+    uint32_t seq0, idle_ticks;
+  };
+  static_assert(sizeof(SvcArgs) == 40, "kernel-argument layout of mi_aql_dropin_svc");
   static const bool host_aql = [] {
     const char *e = getenv("MI_CKSUM_HOST_AQL");
     return !(e && e[0] == '0');
   }();
   AqlDevice *adv = nullptr;
-  bool used_aql = false;
-  if (host_aql && aql_device(c.device, &adv) == 0) {
+  const bool aql = host_aql && aql_device(c.device, &adv) == 0;
+  const bool svc = aql && dropin_svc_on();
+  AqlOne &o = t_aql1;
+  uint32_t prev = 0;
+  // (re)start the service: it serves any sequence word other than seq0
+  auto svc_launch = [&](uint32_t seq0) -> int {
+    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, 0u, c.sout_dev + 16, c.sout_dev, seq0,
+                    dropin_svc_idle_ticks()};
+    int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
+    if (r) return r;
+    o.svc_box = c.sout + 16;
+    o.svc_live = true;
+    return 0;
+  };
+  if (svc) {
+    volatile uint32_t *bx = c.sout + 16;
+    prev = bx[0];
+    bx[1] = 0u;  // cmd: fold
+    bx[2] = (uint32_t)off;
+    bx[3] = len;
+    bx[4] = lanes == MI_SPAN_ABS ? 1u : 0u;
+    bx[5] = pseudo ? 1u : 0u;
+    bx[6] = src;
+    bx[7] = dst;
+    bx[8] = proto;
+    bx[9] = plen;
+    bx[10] = trace ? 1u : 0u;
+    if (!o.svc_live && (rc = svc_launch(prev))) return rc;
+    __atomic_store_n(&c.sout[16], tag, __ATOMIC_RELEASE);
+    if (trace) t_dtrace.t_doorbell = sys_ts();
+  } else if (aql) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
-                        lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst, (uint32_t)proto, plen, tag, c.sout_dev};
+                        lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst, (uint32_t)proto, plen,
+                        tag | (trace ? 0x80000000u : 0u), c.sout_dev};
     // system-scope fences (aql_one_submit): the staging buffer is ordinary
     // (non-coherent) pinned memory rewritten by the host every call, so the
     // GPU's caches must not keep its old lines.  (Round 2's agent-scope opt-in
     // is gone: agent scope is only correct for fine-grained staging.)
     if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false))) return rc;
-    used_aql = true;
   } else {
     hipLaunchKernelGGL(mi_aql_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
                        (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,
-                       (uint32_t)proto, plen, tag, c.sout_dev);
+                       (uint32_t)proto, plen, tag | (trace ? 0x80000000u : 0u), c.sout_dev);
     HIP_TRY(hipGetLastError());
   }
   volatile uint32_t *slot = c.sout;
@@ -4030,11 +4162,12 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
     if ((v >> 16) == tag) break;
     if ((polls & 255u) == 0) {
-      // has the dispatch ended without the word?  (re-read after: the store
-      // and the completion race)
+      // has the work ended without the word?  (re-read after: the store and
+      // the completion race)
       bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
-      if (used_aql) {
-        if (t_aql1.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", t_aql1.error());
+      if (aql) {
+        if (o.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", o.error());
+        if (svc) retired = hsa_signal_load_scacquire(o.sig) == 0;
       } else {
         const hipError_t e = hipStreamQuery(c.sstream);
         if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));
@@ -4042,29 +4175,39 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
       }
       v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
       if ((v >> 16) == tag) break;
-      if (retired) return set_err(-EIO, "scalar fold: the kernel ended without a result");
       if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "scalar fold: no result after 10 s");
+      if (retired && svc) {
+        // the service took its idle exit before this request: a new one
+        o.svc_live = false;
+        o.unretired = false;
+        if ((rc = svc_launch(prev))) return rc;
+        continue;
+      }
+      if (retired) return set_err(-EIO, "scalar fold: the kernel ended without a result");
     }
   }
   *out = (uint16_t)(v & 0xffffu);
-  if (t_dtrace.on && used_aql) {
+  if (trace) {
     t_dtrace.t_seen = sys_ts();
-    // retire the dispatch (its signal) and read its timestamps
-    if ((rc = aql_one_wait(t_aql1))) return rc;
-    hsa_amd_profiling_dispatch_time_t dt{};
-    if (hsa_amd_profiling_get_dispatch_time(t_aql1.dev->agent, t_aql1.sig, &dt) == HSA_STATUS_SUCCESS) {
-      (void)hsa_amd_profiling_convert_tick_to_system_domain(t_aql1.dev->agent, dt.start, &t_dtrace.g_start);
-      (void)hsa_amd_profiling_convert_tick_to_system_domain(t_aql1.dev->agent, dt.end, &t_dtrace.g_end);
+    t_dtrace.g_start = t_dtrace.g_end = 0;
+    uint64_t k0 = 0, k1 = 0;
+    memcpy(&k0, (const void *)(c.sout + 2), 8);
+    memcpy(&k1, (const void *)(c.sout + 4), 8);
+    if (aql && k0 && k1) {
+      (void)hsa_amd_profiling_convert_tick_to_system_domain(o.dev->agent, k0, &t_dtrace.g_start);
+      (void)hsa_amd_profiling_convert_tick_to_system_domain(o.dev->agent, k1, &t_dtrace.g_end);
     }
   }
   return 0;
 }
 
 // Diagnostics (not in the public header): drop-in latency breakdown.
-// mi__dropin_trace(1) switches the calling thread's drop-ins to traced
-// dispatches (completion signal + queue profiling); mi__dropin_trace_read
-// returns, for the last call, in us from fold entry: [doorbell written,
-// kernel start, kernel end, result seen by the host].
+// mi__dropin_trace(1) makes the calling thread's drop-in kernels store their
+// start and end on the GPU's 100 MHz clock (the service: the moment it saw
+// the request and its result store), converted to the HSA system timestamp
+// domain; mi__dropin_trace_read returns, for the last call, in us from fold
+// entry: [doorbell rung / request posted, kernel start, kernel end, result
+// seen by the host].
 int mi__dropin_trace(int on) {
   int rc = ensure_ctx();
   if (rc) return rc;
@@ -4074,8 +4217,6 @@ int mi__dropin_trace(int on) {
       return set_err(-EIO, "no system timestamp frequency");
     t_dtrace.us_per_tick = 1e6 / (double)f;
   }
-  // the queue must have profiling on before the traced dispatches
-  if (on && t_aql1.q) (void)hsa_amd_profiling_set_profiler_enabled(t_aql1.q, 1);
   t_dtrace.on = on != 0;
   return 0;
 }
@@ -4089,6 +4230,20 @@ int mi__dropin_trace_read(double *out, int n) {
   out[3] = us(t.t_seen);
   return 0;
 }
+// Diagnostics / tests (not in the public header): the drop-in service on (1)
+// or off (0) for calls from now on; a thread's running service is stopped by
+// its next call's other path or at thread exit.  Returns the previous setting.
+int mi__set_dropin_service(int on) {
+  const int was = dropin_svc_on() ? 1 : 0;
+  g_dropin_svc.store(on ? 1 : 0);
+  if (!on && t_aql1.svc_live) {
+    int rc = svc_stop(t_aql1);
+    if (rc) return rc;
+  }
+  return was;
+}
+// Is the calling thread's drop-in service running?  (tests)
+int mi__dropin_service_live(void) { return t_aql1.svc_live ? 1 : 0; }
 
 void mi__fatal(const char *what) {
   fprintf(stderr, "libmicksum: %s: %s\n", what, t_err[0] ? t_err : "unknown error");

@@ -19,7 +19,10 @@
  * instead is a wrong checksum.  An embedder may install
  * mi_cksum_set_dropin_error_handler: the handler is told, and the call returns
  * 0xffff -- never the result of verifying a datagram with valid sums (those
- * verify to 0), so an RX caller drops the packet.
+ * verify to 0), so an RX caller drops the packet.  A TX caller (ip_output's
+ * in_cksum_hdr, in_delayed_cksum's in_cksum_skip) stores it into the outgoing
+ * header: with a handler installed a GPU error sends a wrong sum, so a handler
+ * that must not allow that aborts itself (it runs before the value returns).
  */
 #include <stddef.h>
 #include <stdint.h>

@@ -58,3 +58,19 @@ def aligned(a: np.ndarray, align: int = 64):
     v = raw[s:s + a.size]
     v[:] = a
     return raw, v
+
+
+@pytest.fixture(params=["dispatch", "service"])
+def dropin_mode(request):
+    """The (b1) drop-ins as one AQL dispatch per call, or through the thread's
+    resident drop-in service (MI_CKSUM_DROPIN_SERVICE); restored afterwards."""
+    import ctypes as C
+
+    from libunsod_amd._lib import load
+    lib = load()
+    lib.mi__set_dropin_service.restype = C.c_int
+    lib.mi__set_dropin_service.argtypes = [C.c_int]
+    was = lib.mi__set_dropin_service(1 if request.param == "service" else 0)
+    assert was in (0, 1)
+    yield request.param
+    assert lib.mi__set_dropin_service(was) in (0, 1)

@@ -88,10 +88,10 @@ def test_verify_plan_needs_no_gpu():
     buf = torch.zeros(1 << 20, dtype=torch.uint8)
     assert mi.verify_plan(mi.PktBatch(buf, 100, stride=2176, first_off=142, fixed_len=1500)).startswith("k_ipv4_verify<")
     assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=14, fixed_len=46)) == "k_ipv4_verify_slot64"
-    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=30, fixed_len=46)) == "k_ipv4_verify_packed<4>"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, stride=64, first_off=30, fixed_len=46)) == "k_ipv4_verify_packed<4,2 waves>"
     offs = torch.arange(100, dtype=torch.int64) * 300
     lens = torch.full((100,), 280, dtype=torch.int32)
-    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8>"
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_packed<8,2 waves>"
     mi.set_run_kernel(2, 4)
     try:
         assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == "k_ipv4_verify_run_dma<2,4>"

@@ -1,0 +1,161 @@
+"""The drop-in service (VERDICT r3 "do this" 6): a resident workgroup per
+calling thread serves the (b1) drop-ins from a mailbox instead of one queue
+dispatch per call.  Its lifetime rules are what these tests exercise: the
+idle exit and the relaunch by the next call (including a request posted just
+as the service leaves), the stop before any other packet of the thread's queue
+(a host burst), the stop before the staging buffer is reallocated, per-thread
+services across thread churn, and the breakdown stamps.  Every result is
+checked against the reference's known answers or the oracle.
+"""
+import ctypes as C
+import random
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import libunsod_amd as mi
+from libunsod_amd import synth
+from libunsod_amd._lib import load
+from oracle.pyoracle import Oracle
+
+pytestmark = pytest.mark.gpu
+ORC = Oracle("port")
+
+KAT_HDR = bytes.fromhex("450000730000400040110000c0a80001c0a800c7")
+KAT_WANT = {0: 0x61B8, 2: 0x61B8, 1: 0xB861, 3: 0xB861}
+PAT = bytes(i & 0xFF for i in range(1 << 18))
+
+
+@pytest.fixture
+def lib():
+    lib = load()
+    lib.mi__set_dropin_service.restype = C.c_int
+    lib.mi__set_dropin_service.argtypes = [C.c_int]
+    lib.mi__dropin_service_live.restype = C.c_int
+    lib.mi__dropin_trace.argtypes = [C.c_int]
+    lib.mi__dropin_trace_read.argtypes = [C.POINTER(C.c_double), C.c_int]
+    was = lib.mi__set_dropin_service(1)
+    yield lib
+    lib.mi__set_dropin_service(was)
+
+
+def _skip_want(n, skip=0):
+    return ORC.chain_skip([(PAT[:n], 3)], n - skip, skip)
+
+
+def test_service_runs_and_answers(lib):
+    torch.cuda.init()
+    for j in range(200):
+        mod = j % 4
+        assert mi.in_cksum_hdr(KAT_HDR, addr_mod=mod) == KAT_WANT[mod]
+    assert lib.mi__dropin_service_live() == 1
+    m = mi.MbufChain([(PAT[:1500], 3)])
+    assert mi.in_cksum_skip(m, 1500, 0) == 0x4E39  # KAT7
+    assert mi.in_cksum_skip(m, 1480, 20) == _skip_want(1500, 20)
+
+
+def test_service_idle_exit_and_relaunch(lib):
+    """Calls spaced around the 1 ms idle exit: some find the service gone and
+    launch another, some post just as it leaves; all answers right."""
+    rnd = random.Random(7)
+    for j in range(120):
+        mod = j % 4
+        assert mi.in_cksum_hdr(KAT_HDR, addr_mod=mod) == KAT_WANT[mod], j
+        time.sleep(rnd.choice([0.0, 0.0002, 0.0008, 0.001, 0.0012, 0.003]))
+    assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
+
+
+def test_service_stopped_for_host_burst(lib):
+    """A host burst on the same thread goes through the same HSA queue: the
+    service is stopped first (else the burst would wait behind it), and the
+    next drop-in starts a new one."""
+    n, L, stride, first = 64, 1500, 2176, 142
+    b = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=3)
+    raw = np.zeros(b["buf"].size + 4096, np.uint8)
+    s = (-raw.ctypes.data) % 4096
+    buf = raw[s:s + b["buf"].size]
+    buf[:] = b["buf"]
+    ORC.ipv4_finalize_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
+    buf[first + 5 * stride + 99] ^= 0x11
+    want = ORC.ipv4_verify_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
+    mi.host_register(raw)
+    try:
+        for k in range(6):
+            assert mi.in_cksum_hdr(KAT_HDR, addr_mod=k % 4) == KAT_WANT[k % 4]
+            assert lib.mi__dropin_service_live() == 1
+            ip, l4, st, bad = mi.ipv4_verify_host(buf, n, stride=stride, first_off=first, fixed_len=L)
+            assert lib.mi__dropin_service_live() == 0
+            assert np.array_equal(st, want[2]) and np.array_equal(l4, want[1])
+            assert bad == int((want[2] != 0).sum()) >= 1
+    finally:
+        mi.host_unregister(raw)
+
+
+def test_service_staging_growth(lib):
+    """A larger chain than the staging buffer holds: the service is stopped
+    before the buffer is reallocated and restarted on the new one."""
+    sizes = [20, 1500, 65536, 100, 200000, 40, 262144, 64]
+    for n in sizes:
+        m = mi.MbufChain([(PAT[:n // 2], 1), (PAT[n // 2:n], 2)])
+        assert mi.in_cksum_skip(m, n, 0) == ORC.chain_skip([(PAT[:n // 2], 1), (PAT[n // 2:n], 2)], n, 0), n
+        assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
+
+
+def test_service_thread_churn(lib):
+    """16 threads at a time, each with its own service; after they exit the
+    library's queue count is back and nothing was leaked."""
+    lib.mi_cksum_hsa_queues.restype = C.c_int
+    lib.mi__hsa_queues_leaked.restype = C.c_int
+    assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
+    base = lib.mi_cksum_hsa_queues()
+    leaked0 = lib.mi__hsa_queues_leaked()
+    for rnd in range(3):
+        errors = []
+
+        def work(k):
+            try:
+                torch.cuda.set_device(0)
+                for j in range(40):
+                    mod = (k + j) % 4
+                    got = mi.in_cksum_hdr(KAT_HDR, addr_mod=mod)
+                    if got != KAT_WANT[mod]:
+                        errors.append((k, j, hex(got)))
+                m = mi.MbufChain([(PAT[:1500], k % 64)])
+                if mi.in_cksum_skip(m, 1500, 0) != 0x4E39:
+                    errors.append((k, "skip"))
+            except Exception as e:  # noqa: BLE001
+                errors.append((k, repr(e)))
+
+        ts = [threading.Thread(target=work, args=(k,)) for k in range(16)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in ts)
+        assert not errors, errors[:5]
+        assert lib.mi_cksum_hsa_queues() == base, rnd
+    assert lib.mi__hsa_queues_leaked() == leaked0
+
+
+@pytest.mark.parametrize("service", [0, 1])
+def test_breakdown_stamps(lib, service):
+    """The breakdown's four times are ordered: request posted, kernel start
+    (the service: request seen), kernel end, result seen -- within the slack
+    of the clock conversion."""
+    lib.mi__set_dropin_service(service)
+    out = (C.c_double * 4)()
+    assert lib.mi__dropin_trace(1) == 0
+    try:
+        rows = []
+        for j in range(50):
+            assert mi.in_cksum_hdr(KAT_HDR, addr_mod=j % 4) == KAT_WANT[j % 4]
+            assert lib.mi__dropin_trace_read(out, 4) == 0
+            rows.append(list(out))
+    finally:
+        lib.mi__dropin_trace(0)
+    r = np.median(np.array(rows), axis=0)
+    assert 0 <= r[0] <= r[3] and r[1] <= r[2] <= r[3] + 1.0, r
+    assert r[1] >= r[0] - 1.0, r

@@ -27,7 +27,7 @@ def cpu(t):
 
 
 # ------------------------------------------------- (b1) drop-ins vs golden
-def test_dropin_skip_golden(golden):
+def test_dropin_skip_golden(golden, dropin_mode):
     g = golden
     bad = []
     for k in range(len(g["sk_result"])):
@@ -38,7 +38,7 @@ def test_dropin_skip_golden(golden):
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
 
 
-def test_dropin_pseudo_golden(golden):
+def test_dropin_pseudo_golden(golden, dropin_mode):
     g = golden
     bad = []
     for k in range(len(g["ps_result"])):
@@ -50,7 +50,7 @@ def test_dropin_pseudo_golden(golden):
     assert not bad, f"{len(bad)} mismatches, first {bad[:5]}"
 
 
-def test_dropin_hdr_golden(golden):
+def test_dropin_hdr_golden(golden, dropin_mode):
     g = golden
     for k in range(len(g["hd_result"])):
         off = int(g["hd_off"][k])
@@ -529,7 +529,7 @@ def test_slot64_edge_cases(first):
             h[p + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(8)))
     buf = dev_tensor(h)
     b = mi.PktBatch(buf, n, stride=stride, first_off=first, fixed_len=L)
-    assert mi.verify_plan(b) == ("k_ipv4_verify_slot64" if first < 16 else "k_ipv4_verify_packed<4>")
+    assert mi.verify_plan(b) == ("k_ipv4_verify_slot64" if first < 16 else "k_ipv4_verify_packed<4,2 waves>")
     r = mi.ipv4_verify(b, bad_count=True)
     ip, l4, st = ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
     assert np.array_equal(cpu(r["ip"]), ip) and np.array_equal(cpu(r["l4"]), l4)
@@ -685,14 +685,11 @@ def test_offs32_same_results(golden, layout):
     assert np.array_equal(cpu(gbuf), g["fin_out"])
 
 
-@pytest.mark.parametrize("dyn", ["0", "1"])
 @pytest.mark.parametrize("shape", ["", "8x12"])
-def test_verify_multi_matches_single(shape, dyn, monkeypatch):
+def test_verify_multi_matches_single(shape):
     """mi_cksum_ipv4_verify_multi == mi_cksum_ipv4_verify per batch: slot
     batches of several lengths (merged into one launch), a packed batch (its
-    own launch), empty and one-packet batches, corrupted datagrams -- with the
-    static grid stride and with dynamic unit scheduling (MI_CKSUM_MULTI_DYN)."""
-    monkeypatch.setenv("MI_CKSUM_MULTI_DYN", dyn)
+    own launch), empty and one-packet batches, corrupted datagrams."""
     if shape:
         mi.set_shape(*[int(x) for x in shape.split("x")])
     try:
@@ -737,36 +734,6 @@ def test_verify_multi_matches_single(shape, dyn, monkeypatch):
         assert int(bad.item()) == nbad
     finally:
         mi.set_shape(0, 0, 0)
-
-
-def test_verify_multi_dynamic_counters_reset(monkeypatch):
-    """Dynamic unit scheduling: 150 multi-batch launches in a row (more than
-    the thread's 64 counter pairs, so every pair is reused after its last wave
-    reset it), alternating over two streams, outputs rewritten every time."""
-    monkeypatch.setenv("MI_CKSUM_MULTI_DYN", "1")
-    n, L, stride, first = 4000, 1500, 2176, 142
-    b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=12)
-    h = b0["buf"]
-    ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
-    h[first + 17 * stride + 100] ^= 0x40
-    want = ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
-    bs = [mi.PktBatch(dev_tensor(h), n, stride=stride, first_off=first, fixed_len=L) for _ in range(3)]
-    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
-    outs = [[dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"),
-                  l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
-                  status=torch.zeros(n, dtype=torch.uint8, device="cuda")) for _ in bs] for _ in streams]
-    torch.cuda.synchronize()
-    for k in range(150):
-        q = k % 2
-        with torch.cuda.stream(streams[q]):
-            for o in outs[q]:
-                o["status"].fill_(0xFF)
-            mi.ipv4_verify_multi(bs, outs[q], stream=streams[q])
-        if k % 25 == 24:
-            torch.cuda.synchronize()
-            for o in outs[0] + outs[1]:
-                assert np.array_equal(cpu(o["status"]), want[2]) and np.array_equal(cpu(o["l4"]), want[1])
-    torch.cuda.synchronize()
 
 
 def test_repeat_handle_outputs_and_rotation():

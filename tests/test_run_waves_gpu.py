@@ -27,13 +27,13 @@ def _set_waves(w):
     assert lib.mi__set_run_waves(w) == 0
 
 
-@pytest.fixture(params=[1, 2], ids=lambda w: f"{w}wave")
+@pytest.fixture(params=[1, 4], ids=lambda w: f"{w}wave")
 def run_waves(request):
     _set_waves(request.param)
     try:
         yield request.param
     finally:
-        _set_waves(4)
+        _set_waves(2)
 
 
 def test_plan_names_the_workgroup(run_waves):

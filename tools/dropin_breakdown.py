@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Where the ~8 us of a (b1) drop-in call goes (VERDICT r3 "do this" 6).
 
-With mi__dropin_trace(1) the calling thread's drop-in dispatches carry a
-completion signal and queue profiling, and every call records, in the HSA
-system timestamp domain, from the fold's entry: the doorbell written, the
-kernel's start and end (AQL dispatch timestamps converted to the system
-domain), and the moment the host sees the result word.  Median over N calls of
-each (b1) function on real mbuf chains, next to the untraced per-call time
-(the traced dispatch's signal costs a little, so the phases are shares).
+With mi__dropin_trace(1) the drop-in kernel stores its start and end on the
+GPU's 100 MHz clock next to the result (the drop-in service: the moment it saw
+the request, and its result store), converted to the HSA system timestamp
+domain; every call then records, from the fold's entry: the doorbell rung (the
+service: the request posted), the kernel's start and end, and the moment the
+host sees the result word.  Median over N calls of each (b1) function on real
+mbuf chains, next to the untraced per-call time, for one dispatch per call and
+for the resident drop-in service.
 
     python tools/dropin_breakdown.py [--calls 400] > dropin_breakdown.jsonl
 """
@@ -36,6 +37,8 @@ def main():
     lib = mi.load()
     lib.mi__dropin_trace.argtypes = [C.c_int]
     lib.mi__dropin_trace_read.argtypes = [C.POINTER(C.c_double), C.c_int]
+    lib.mi__set_dropin_service.restype = C.c_int
+    lib.mi__set_dropin_service.argtypes = [C.c_int]
     pat = bytes(i & 0xFF for i in range(65536))
     m64 = mi.MbufChain([pat])
     ip_hdr = bytes.fromhex("450005dc0000400040060000c0a80101c0a80102")
@@ -51,7 +54,8 @@ def main():
         "in_cksum_skip_65536B": (lib.in_cksum_skip, (C.c_void_p(m64.ptr), 65536, 0)),
     }
     out = (C.c_double * 4)()
-    for name, (fn, args) in cases.items():
+    for (name, (fn, args)), mode in [(c, m) for m in ("dispatch", "service") for c in cases.items()]:
+        lib.mi__set_dropin_service(1 if mode == "service" else 0)
         fn(*args)
         plain = []
         for _ in range(a.calls):
@@ -71,14 +75,16 @@ def main():
         r = np.array(rows)
         med = lambda x: round(float(np.median(x)), 3)  # noqa: E731
         print(json.dumps(dict(
-            call=name, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6), traced_call_us=med(np.array(tot) * 1e6),
+            call=name, mode=mode, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6), traced_call_us=med(np.array(tot) * 1e6),
             entry_to_doorbell_us=med(r[:, 0]),
             doorbell_to_kernel_start_us=med(r[:, 1] - r[:, 0]),
             kernel_us=med(r[:, 2] - r[:, 1]),
             kernel_start_to_result_seen_us=med(r[:, 3] - r[:, 1]),
+            kernel_end_to_result_seen_us=med(r[:, 3] - r[:, 2]),
             entry_to_result_seen_us=med(r[:, 3]),
             note="system-domain timestamps from the fold's entry (after the mbuf walk and staging copy); "
                  "call_us = the whole ctypes call measured in Python")), flush=True)
+    lib.mi__set_dropin_service(0)
 
 
 if __name__ == "__main__":

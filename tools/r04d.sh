@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 O=gpurun_out/r04d; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "tx" > $O/gpu_tests_tx.log 2>&1 || { tail -30 $O/gpu_tests_tx.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread -k "tx or verify_multi" > $O/gpu_tests_tx.log 2>&1 || { tail -30 $O/gpu_tests_tx.log; exit 1; }
 tail -1 $O/gpu_tests_tx.log
 for r in 0 1; do
   for k in pair wave; do
@@ -21,4 +21,8 @@ timeout -k 10 300 python -u tools/grid_iso.py --config 1500 --caps 1024,1280,204
 cut -c1-250 $O/grid_iso.jsonl
 timeout -k 10 120 python -u tools/dropin_breakdown.py --calls 400 > $O/dropin_breakdown.jsonl 2> $O/dropin.err || exit 1
 cut -c1-300 $O/dropin_breakdown.jsonl
+for r in 0 1; do for d in 0 1; do
+  MI_CKSUM_MULTI_DYN=$d timeout -k 10 200 python -u tools/bench_multi.py --ms 4,16 --shapes auto,16x6 | sed "s/^{/{\"dyn\": $d, \"round\": $r, /" >> $O/multi_dyn.jsonl || exit 1
+done; done
+cut -c1-220 $O/multi_dyn.jsonl
 echo done
