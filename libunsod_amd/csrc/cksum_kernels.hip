@@ -2289,9 +2289,10 @@ int aql_device(int dev, AqlDevice **out) {
         (void)ldr.hsa_ven_amd_loader_iterate_executables(aql_exe_cb, &f);
       for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
         if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
-        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : kAqlHidden + 66u) || a.k[i].kernarg > 512u)
+        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 40u : kAqlHidden + 66u) ||
+                 a.k[i].kernarg > 512u)
           fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
-               i == kAqlScalar ? 56u : (unsigned)sizeof(AqlArgs));
+               i == kAqlScalar ? 56u : i == kAqlSvc ? 40u : (unsigned)sizeof(AqlArgs));
       }
     }
   }
