@@ -549,11 +549,13 @@ def plumbing_64k(seconds: float = 1.0) -> dict:
 
 def dropin_latency(mi, calls: int = 400) -> dict:
     """(b1) drop-in cost per call on this host: libmicksum's in_cksum_hdr /
-    in_cksum_pseudo_header / in_cksum_skip (one GPU launch each, the bytes
-    read over PCIe from pinned staging) against the reference's own functions
-    (oracle/_ref) on the same real mbuf chains.  Median over `calls` calls
-    through ctypes; ``ctypes_floor_us`` is the same loop around in_addword
-    (no checksum work) and is included in every figure."""
+    in_cksum_pseudo_header / in_cksum_skip (the bytes read over PCIe from
+    pinned staging; one AQL dispatch per call, and through the thread's
+    resident drop-in service -- ``gpu_dropin_us`` is the library's default
+    mode) against the reference's own functions (oracle/_ref) on the same real
+    mbuf chains.  Median over `calls` calls through ctypes; ``ctypes_floor_us``
+    is the same loop around in_addword (no checksum work) and is included in
+    every figure."""
     import ctypes as C
     from oracle.pyoracle import Oracle, available
     lib = mi.load()
@@ -593,9 +595,26 @@ def dropin_latency(mi, calls: int = 400) -> dict:
         ref.ref_in_cksum_pseudo_header.restype = C.c_uint16
         ref.ref_in_cksum_pseudo_header.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_uint32, C.c_uint32,
                                                    C.c_uint8]
+    lib.mi__set_dropin_service.restype = C.c_int
+    lib.mi__set_dropin_service.argtypes = [C.c_int]
+    default_mode = lib.mi__set_dropin_service(0)  # (returns the setting it replaces)
+    lib.mi__set_dropin_service(default_mode)
+    out["default_mode"] = "service" if default_mode else "dispatch"
+
+    def both(g, args):
+        # one AQL dispatch per call, and the thread's resident drop-in service
+        r = {}
+        for mode, on in (("dispatch", 0), ("service", 1)):
+            lib.mi__set_dropin_service(on)
+            r[mode] = med(g, args)
+        lib.mi__set_dropin_service(default_mode)
+        return r
+
     for name, (fn, args) in cases.items():
         g = getattr(lib, fn)
-        row = dict(gpu_dropin_us=med(g, args))
+        modes = both(g, args)
+        row = dict(gpu_dropin_us=modes[out["default_mode"]], gpu_dispatch_us=modes["dispatch"],
+                   gpu_service_us=modes["service"])
         if ref is not None:
             r = getattr(ref, "ref_" + fn)
             assert int(g(*args)) == int(r(*args)), f"{fn}: drop-in differs from the reference"

@@ -4190,14 +4190,14 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   *out = (uint16_t)(v & 0xffffu);
   if (trace) {
     t_dtrace.t_seen = sys_ts();
-    t_dtrace.g_start = t_dtrace.g_end = 0;
     uint64_t k0 = 0, k1 = 0;
     memcpy(&k0, (const void *)(c.sout + 2), 8);
     memcpy(&k1, (const void *)(c.sout + 4), 8);
-    if (aql && k0 && k1) {
-      (void)hsa_amd_profiling_convert_tick_to_system_domain(o.dev->agent, k0, &t_dtrace.g_start);
-      (void)hsa_amd_profiling_convert_tick_to_system_domain(o.dev->agent, k1, &t_dtrace.g_end);
-    }
+    // (the kernel's own duration on the GPU's 100 MHz clock: that clock's
+    // conversion to the host's domain was measured to be off by 10-20 us, so
+    // only its differences are used)
+    t_dtrace.g_start = k0;
+    t_dtrace.g_end = k1 >= k0 ? k1 : k0;
   }
   return 0;
 }
@@ -4205,10 +4205,10 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
 // Diagnostics (not in the public header): drop-in latency breakdown.
 // mi__dropin_trace(1) makes the calling thread's drop-in kernels store their
 // start and end on the GPU's 100 MHz clock (the service: the moment it saw
-// the request and its result store), converted to the HSA system timestamp
-// domain; mi__dropin_trace_read returns, for the last call, in us from fold
-// entry: [doorbell rung / request posted, kernel start, kernel end, result
-// seen by the host].
+// the request, and its result store); mi__dropin_trace_read returns, for the
+// last call: [doorbell rung / request posted (us from fold entry, host
+// clock), the kernel's own time (us, GPU clock; -1 if not recorded), result
+// seen by the host (us from fold entry), 0].
 int mi__dropin_trace(int on) {
   int rc = ensure_ctx();
   if (rc) return rc;
@@ -4226,9 +4226,9 @@ int mi__dropin_trace_read(double *out, int n) {
   const DropinTrace &t = t_dtrace;
   auto us = [&](uint64_t x) { return x ? ((double)x - (double)t.t_entry) * t.us_per_tick : -1.0; };
   out[0] = us(t.t_doorbell);
-  out[1] = us(t.g_start);
-  out[2] = us(t.g_end);
-  out[3] = us(t.t_seen);
+  out[1] = t.g_start ? (double)(t.g_end - t.g_start) * 0.01 : -1.0;  // 100 MHz
+  out[2] = us(t.t_seen);
+  out[3] = 0.0;
   return 0;
 }
 // Diagnostics / tests (not in the public header): the drop-in service on (1)

@@ -501,7 +501,10 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       k1_c = k1_n;
     };
     const uint32_t l3 = t.l3;
-    const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
+    uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
+    // (opaque: the compiler would otherwise carry values derived from D from
+    // frame to frame, two more live VGPRs across the pass loop)
+    asm volatile("" : "+v"(D));
     const uint32_t h = D & 15u, c0 = D & ~15u;
     uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
     // walk 1: bytes in the chain, the IP mbuf (segment holding frame byte l3)

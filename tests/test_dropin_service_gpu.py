@@ -136,15 +136,18 @@ def test_service_thread_churn(lib):
             t.join(timeout=60)
         assert not any(t.is_alive() for t in ts)
         assert not errors, errors[:5]
-        assert lib.mi_cksum_hsa_queues() == base, rnd
+        # (Python's join returns before the OS thread has run its key destructors)
+        deadline = time.monotonic() + 5.0
+        while lib.mi_cksum_hsa_queues() != base and time.monotonic() < deadline:
+            time.sleep(0.01)
+        assert lib.mi_cksum_hsa_queues() == base, (rnd, lib.mi_cksum_hsa_queues(), base)
     assert lib.mi__hsa_queues_leaked() == leaked0
 
 
 @pytest.mark.parametrize("service", [0, 1])
 def test_breakdown_stamps(lib, service):
-    """The breakdown's four times are ordered: request posted, kernel start
-    (the service: request seen), kernel end, result seen -- within the slack
-    of the clock conversion."""
+    """The breakdown's figures are consistent: request posted before the
+    result is seen, and the kernel's own time (GPU clock) inside that span."""
     lib.mi__set_dropin_service(service)
     out = (C.c_double * 4)()
     assert lib.mi__dropin_trace(1) == 0
@@ -157,5 +160,5 @@ def test_breakdown_stamps(lib, service):
     finally:
         lib.mi__dropin_trace(0)
     r = np.median(np.array(rows), axis=0)
-    assert 0 <= r[0] <= r[3] and r[1] <= r[2] <= r[3] + 1.0, r
-    assert r[1] >= r[0] - 1.0, r
+    assert 0 <= r[0] <= r[2], r
+    assert 0 < r[1] <= r[2] - r[0], r

@@ -3,10 +3,10 @@
 
 With mi__dropin_trace(1) the drop-in kernel stores its start and end on the
 GPU's 100 MHz clock next to the result (the drop-in service: the moment it saw
-the request, and its result store), converted to the HSA system timestamp
-domain; every call then records, from the fold's entry: the doorbell rung (the
-service: the request posted), the kernel's start and end, and the moment the
-host sees the result word.  Median over N calls of each (b1) function on real
+the request, and its result store); every call then records, on the host's
+clock from the fold's entry, the doorbell rung (the service: the request
+posted) and the moment the host sees the result word, and the kernel's own
+time from the GPU clock's difference.  Median over N calls of each (b1) function on real
 mbuf chains, next to the untraced per-call time, for one dispatch per call and
 for the resident drop-in service.
 
@@ -75,15 +75,17 @@ def main():
         r = np.array(rows)
         med = lambda x: round(float(np.median(x)), 3)  # noqa: E731
         print(json.dumps(dict(
-            call=name, mode=mode, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6), traced_call_us=med(np.array(tot) * 1e6),
-            entry_to_doorbell_us=med(r[:, 0]),
-            doorbell_to_kernel_start_us=med(r[:, 1] - r[:, 0]),
-            kernel_us=med(r[:, 2] - r[:, 1]),
-            kernel_start_to_result_seen_us=med(r[:, 3] - r[:, 1]),
-            kernel_end_to_result_seen_us=med(r[:, 3] - r[:, 2]),
-            entry_to_result_seen_us=med(r[:, 3]),
-            note="system-domain timestamps from the fold's entry (after the mbuf walk and staging copy); "
-                 "call_us = the whole ctypes call measured in Python")), flush=True)
+            call=name, mode=mode, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6),
+            traced_call_us=med(np.array(tot) * 1e6),
+            entry_to_posted_us=med(r[:, 0]),
+            posted_to_result_seen_us=med(r[:, 2] - r[:, 0]),
+            kernel_own_us=med(r[:, 1]),
+            outside_kernel_us=med(r[:, 2] - r[:, 0] - r[:, 1]),
+            note="host clock from the fold's entry (after the mbuf walk and staging copy); kernel_own_us on the "
+                 "GPU's 100 MHz clock (dispatch: kernel start to result store; service: request seen to result "
+                 "store); outside_kernel_us = doorbell/posting to result seen minus the kernel's own time = queue "
+                 "dispatch + wave launch (dispatch) or mailbox poll (service) + result visibility; call_us = the "
+                 "whole ctypes call measured in Python")), flush=True)
     lib.mi__set_dropin_service(0)
 
 

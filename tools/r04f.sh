@@ -10,7 +10,7 @@ tail -1 $O/gpu_tests_dropin.log
 timeout -k 10 180 python -u tools/dropin_breakdown.py --calls 400 > $O/dropin_breakdown.jsonl 2> $O/dropin.err || { tail $O/dropin.err; exit 1; }
 cut -c1-420 $O/dropin_breakdown.jsonl
 for r in 0 1; do
-  for v in base tx4 tx5; do
+  for v in base tx4 tx5 tx5b; do
     for lay in socket single; do
       MI_CKSUM_LIB=tools/ab/libmicksum_$v.so timeout -k 10 120 python -u tools/bench_tx.py --layout $lay --steps 200 --cpu-seconds 0 $([ $r = 0 ] && echo --check) \
         | sed "s/^{/{\"lib\": \"$v\", \"round\": $r, /" >> $O/tx_lds_ab.jsonl || exit 1
