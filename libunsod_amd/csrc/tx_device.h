@@ -303,11 +303,9 @@ __device__ __forceinline__ TxCut tx_cut(const TxSegs &g, uint32_t ci, uint32_t h
   return c;
 }
 // The chunk from its (at most two) loads: one mask per dword in the common
-// case, byte masks at the frame's ends (L: the frame length), byte loads in
-// the rare slow case -- which reads the segment table (S0..S3, D0..D3) from
-// the group's LDS row, so that it is not live in VGPRs across the loads.
-__device__ __forceinline__ u32x4 tx_build(int L, const u32x4 *sgrow, const TxCut &c, const u32x4 &xa,
-                                          const u32x4 &xb, __amdgpu_buffer_rsrc_t rs) {
+// case, byte masks at the frame's ends, byte loads in the rare slow case.
+__device__ __forceinline__ u32x4 tx_build(const TxSegs &g, const TxCut &c, const u32x4 &xa, const u32x4 &xb,
+                                          __amdgpu_buffer_rsrc_t rs) {
   u32x4 v{0, 0, 0, 0};
   if (!c.clip && !c.slow) {
     // bytes [0, B) from xa, [B, 16) from xb
@@ -319,13 +317,12 @@ __device__ __forceinline__ u32x4 tx_build(int L, const u32x4 *sgrow, const TxCut
     v.z = (xa.z & (uint32_t)hm) | (xb.z & ~(uint32_t)hm);
     v.w = (xa.w & (uint32_t)(hm >> 32)) | (xb.w & ~(uint32_t)(hm >> 32));
   } else if (!c.slow) {
-    const int lo = max(c.q0, 0) - c.q0, hi = min(c.q0 + 16, L) - c.q0;
+    const int lo = max(c.q0, 0) - c.q0, hi = min(c.q0 + 16, g.L) - c.q0;
     merge_bytes(v, xa, lo, min(c.B, hi));
     if (c.two) merge_bytes(v, xb, c.B, hi);
   } else {
-    const u32x4 S = sgrow[0], Dl = sgrow[1];
-    for (int q = max(c.q0, 0); q < min(c.q0 + 16, L); ++q) {
-      const uint32_t d = q >= (int)S.w ? Dl.w : q >= (int)S.z ? Dl.z : q >= (int)S.y ? Dl.y : Dl.x;
+    for (int q = max(c.q0, 0); q < min(c.q0 + 16, g.L); ++q) {
+      const uint32_t d = q >= g.S3 ? g.D3 : q >= g.S2 ? g.D2 : q >= g.S1 ? g.D1 : g.D0;
       put_byte(v, q - c.q0, __builtin_amdgcn_raw_buffer_load_b8(rs, (uint32_t)(q + (int)d), 0, 0));
     }
   }
@@ -433,19 +430,10 @@ __device__ __forceinline__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffe
 // prefetch costs ~10 and a few spill to scratch): profiles/tx_copy_r02.jsonl,
 // socket frames 59-64 us per launch against 64-66 without the prefetch and
 // 69 with it at 3 waves per SIMD.
-#ifndef MI_TXC_WAVES
-#define MI_TXC_WAVES 4
-#endif
 template <int G, int U>
-__global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy(TxDesc t) {
+__global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) {
   static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
   __shared__ uint32_t s_seg[kBlock / G][kTxSeg][2];
-  // Parked in LDS instead of VGPRs through the pass loop (MI_TXC_LDS): each
-  // lane's held header chunk, and the group's segment table in the form
-  // tx_cut reads it (S0..S3, D0..D3), re-read every pass.
-  __shared__ u32x4 s_held[kBlock];
-  __shared__ u32x4 s_sg[kBlock / G][2];
-  __shared__ uint32_t s_pf[5][kBlock];  // the next frame's descriptors, across the generic path
   Desc ds{}, dd{};
   ds.base = t.src;
   ds.bytes = t.src_bytes;
@@ -501,10 +489,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       k1_c = k1_n;
     };
     const uint32_t l3 = t.l3;
-    uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
-    // (opaque: the compiler would otherwise carry values derived from D from
-    // frame to frame, two more live VGPRs across the pass loop)
-    asm volatile("" : "+v"(D));
+    const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
     const uint32_t h = D & 15u, c0 = D & ~15u;
     uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
     // walk 1: bytes in the chain, the IP mbuf (segment holding frame byte l3)
@@ -536,13 +521,14 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
     }
     ip_mlen = group_lane<G>(ip_mlen, 0);
     const bool odd = (h + l3) & 1u;  // parity of the IP header's destination address
+    IpHdr ih{};
     bool ok = false, do_ip = false, do_l4 = false, udp = false, done = false;
     uint32_t at = 0;
     int hend = 0, lend = 0;
     uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
     auto decide1 = [&](const u32x4 &h0, uint32_t hoff) {
       const u32x4 hv[1] = {h0};
-      const IpHdr ih = parse_ipv4<G, 1>(hv, hoff);  // parsed again from s_held at the end
+      ih = parse_ipv4<G, 1>(hv, hoff);
       const TxPlan pl = tx_plan(t, i, len, ih);
       ok = pl.ok;
       do_ip = pl.do_ip;
@@ -552,13 +538,11 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       hend = pl.hend;
       lend = pl.lend;
     };
-    // (the header's own sums -- IP options -- come from the held chunks at the
-    // end: every header byte is in them, or the frame takes the generic path)
     auto fold_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t p) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int rel = (int)(16u * (cfirst + p * (G * U) + u * G + lane)) - (int)(h + l3);
-        fold_chunk(v[u], rel, lend, hend, false, acc_t, acc_h, acc_f);
+        fold_chunk(v[u], rel, lend, hend, hend > 20, acc_t, acc_h, acc_f);
       }
     };
     auto store_all = [&](const u32x4 (&v)[U], uint32_t cfirst, uint32_t clast, uint32_t p, int pa, int pe,
@@ -584,24 +568,15 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       const uint32_t npass = (nch + G * U - 1) / (G * U);
       // Chunk ci of the frame is gathered from at most two loads (tx_cut,
       // tx_build above).
+      const int S1 = seg_start(1), S2 = seg_start(2), S3 = seg_start(3);
+      const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
       const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
-      if (lane < 4) {
-        ((uint32_t *)&s_sg[grp][0])[lane] = lane ? (uint32_t)seg_start(lane) : 0u;
-        ((uint32_t *)&s_sg[grp][1])[lane] = seg_delta(lane);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
+      u32x4 held{0, 0, 0, 0};
       for (uint32_t p = 0; p < npass; ++p) {
         u32x4 v[U];
         u32x4 xa[U], xb[U];
         TxCut cut[U];
-        // the segment table from LDS every pass (an index the compiler cannot
-        // see is loop-invariant, so the reads are not hoisted into registers)
-        uint32_t z;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-        const u32x4 sS = s_sg[grp + z][0], sD = s_sg[grp + z][1];
-        const TxSegs sg{(int)sS.y, (int)sS.z, (int)sS.w, (int)len, sD.x, sD.y, sD.z, sD.w, lim};
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
@@ -611,15 +586,15 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
         }
         if (p == 0) prefetch2();
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = tx_build((int)len, &s_sg[grp][0], cut[u], xa[u], xb[u], rs);
+        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
           const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-          const uint32_t need = max(max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u), hend > 20 ? l3 + hend : 0u);
+          const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
           if ((uint64_t)need + h > 16ull * G) break;  // a sum field beyond the held chunks: generic path
           done = true;
-          s_held[threadIdx.x] = v[0];
+          held = v[0];
         }
         fold_all(v, 0, p);
         store_all(v, 0, nch, p, 0, (int)len, p == 0 ? 1 : 0);
@@ -630,19 +605,6 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       }
       if (done) {
         const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
-        u32x4 held = npass ? s_held[threadIdx.x] : u32x4{0, 0, 0, 0};
-        IpHdr ih{};
-        if (npass) {
-          const u32x4 hv[1] = {held};
-          ih = parse_ipv4<G, 1>(hv, h + l3);
-          if (hend > 20) {
-            const int rel = (int)(16u * lane) - (int)(h + l3);
-            if (rel < hend) {
-              acc_h = range_sum(held, rel, 0, hend);
-              acc_f = range_sum(held, rel, 10, 12);
-            }
-          }
-        }
         uint32_t c_ip, c_l4;
         tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
         const uint32_t pip = l3 + 10u, pl4 = l3 + at;
@@ -664,24 +626,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? MI_TXC_WAVES : 1)) void k_tx_copy
       __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
     }
     prefetch2();
-    if (!done) {
-      // the generic path needs the registers: the next frame's prefetched
-      // descriptors wait in LDS (read back through an index the compiler
-      // cannot see through, so the values are not kept live across it)
-      s_pf[0][threadIdx.x] = len_c;
-      s_pf[1][threadIdx.x] = k0_c;
-      s_pf[2][threadIdx.x] = k1_c;
-      s_pf[3][threadIdx.x] = (uint32_t)sl_c;
-      s_pf[4][threadIdx.x] = so_c;
-      tx_frame_generic<G, 1>(t, rs, rd, i, lane, len, t.pkt_seg[i], t.pkt_seg[i + 1], ip_mlen);
-      uint32_t z;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-      len_c = s_pf[0][threadIdx.x + z];
-      k0_c = s_pf[1][threadIdx.x + z];
-      k1_c = s_pf[2][threadIdx.x + z];
-      sl_c = (int32_t)s_pf[3][threadIdx.x + z];
-      so_c = s_pf[4][threadIdx.x + z];
-    }
+    if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
   }
 }
 
