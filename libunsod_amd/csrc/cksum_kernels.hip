@@ -44,6 +44,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <hsa/hsa_ven_amd_loader.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -1426,6 +1427,23 @@ __device__ __forceinline__ uint32_t scalar_span(const uint8_t *base, uint32_t by
 }
 }  // namespace
 
+// The tagged result word, and with tracing the kernel's two clock stamps
+// before it (out[2..5]).  Nothing before the result needs to be visible to
+// the host first -- every read of the staging bytes has been consumed -- so
+// the untraced store is relaxed (a release at system scope would write back
+// the whole L2 first); the traced one orders the stamps before it.
+__device__ __forceinline__ void scalar_result(uint32_t *out, uint32_t tag, uint32_t res, bool trace, uint64_t t0) {
+  const uint32_t w = ((tag & 0xffffu) << 16) | res;
+  if (trace) {
+    const uint64_t t1 = rt_clock();
+    __hip_atomic_store((uint64_t *)(out + 2), t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((uint64_t *)(out + 4), t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+    __hip_atomic_store(out, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // (the same kernel serves the HIP launch and the AQL one-shot dispatch, hence
 // extern "C").  tag bit 31: also store the kernel's start and end on the
 // 100 MHz clock at out[2..5] (the drop-in latency breakdown).
@@ -1436,42 +1454,39 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
   const uint64_t t0 = rt_clock();
   __shared__ uint32_t part[kScalarThreads / 64];
   const uint32_t res = scalar_span(base, bytes, off, len, abs_lanes, (uint32_t)pseudo, src, dst, proto, plen, part);
-  if (threadIdx.x == 0) {
-    if (tag >> 31) {
-      const uint64_t t1 = rt_clock();
-      __hip_atomic_store((uint64_t *)(out + 2), t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store((uint64_t *)(out + 4), t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __hip_atomic_store(out, ((tag & 0xffffu) << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (threadIdx.x == 0) scalar_result(out, tag, res, (tag >> 31) != 0u, t0);
 }
 
 // The drop-in service (MI_CKSUM_DROPIN_SERVICE): one workgroup that stays
 // resident while its thread keeps calling drop-ins, so a call costs no queue
-// dispatch -- the host writes the request into a mailbox in coherent
-// page-locked memory (box[1..10]: cmd, off, len, abs_lanes, pseudo, src, dst,
-// proto, plen, trace; then box[0], the request's sequence word, with release
-// order),
-// lane 0 polls box[0] with system-scope loads, the workgroup folds the span and
-// stores the tagged result as mi_aql_scalar does.  Exit conditions every wave
-// reaches: a stop request (cmd 1), or no new request for idle_ticks of the
-// 100 MHz clock -- the host sees the dispatch retire (its completion signal)
-// and launches a new one when the next call comes.  With trace set, out[2..5]
-// get the clock at the moment the request was seen and at the result store.
+// dispatch.  The host writes the request into a mailbox -- fine-grained
+// device memory written through the PCIe BAR when the platform maps it for the
+// CPU, else coherent page-locked host memory: box[1..11] = cmd, off, len,
+// abs_lanes, pseudo, src, dst, proto, plen, trace, inline; a span of at most
+// kSvcInlineBytes bytes (with its staging offset) at box[kSvcInline..], else
+// the span stays in the page-locked staging buffer; then box[0], the request's
+// sequence word, last.  Lane 0 polls box[0]; once it moves, ONE round trip
+// brings the fields (lanes 1..11) and the inline span (lanes 16..31), and an
+// inline span is folded by wave 0 alone; a staged one by the whole workgroup
+// (scalar_span).  The result goes to the caller's pinned word as mi_aql_scalar
+// stores it.  Exit conditions every wave reaches: a stop request (cmd 1), or
+// no new request for idle_ticks of the 100 MHz clock -- the host sees the
+// dispatch retire (its completion signal) and launches a new one when the next
+// call comes.  With trace set, out[2..5] get the clock at the moment the
+// request was seen and at the result store.
+constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 256, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
                                                                              const uint32_t *box, uint32_t *out,
                                                                              uint32_t seq0, uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
-  __shared__ uint32_t req[11];
+  __shared__ uint32_t req[13];  // [0] sequence, [1..11] fields, [12] served by wave 0
   uint32_t last = seq0;
-  uint64_t t_last = rt_clock();
+  uint64_t t_last = rt_clock(), t_seen = 0;
   for (;;) {
     if (threadIdx.x < 64) {
-      // wave 0: lane 0 polls the sequence word; once it moves, lanes 1..10
-      // read the request's fields with ONE load instruction (one PCIe round
-      // trip -- ten dependent loads into one register were measured at ~14 us)
+      const uint32_t lane = threadIdx.x;
       uint32_t sq = last;
-      if (threadIdx.x == 0) {
+      if (lane == 0) {
         for (;;) {
           sq = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           if (sq != last || rt_clock() - t_last > idle_ticks) break;
@@ -1479,34 +1494,62 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
         }
       }
       sq = __builtin_amdgcn_readfirstlane(sq);
+      uint32_t served = 0;
       if (sq != last) {
+        t_seen = rt_clock();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (threadIdx.x >= 1 && threadIdx.x < 11)
-          req[threadIdx.x] = __hip_atomic_load(box + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t f = 0;
+        u32x4 v{0, 0, 0, 0};
+        if (lane >= 1 && lane < 12) f = __hip_atomic_load(box + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane >= 16 && lane < 32) {
+          const uint32_t *q = box + kSvcInline + 4u * (lane - 16u);
+          v.x = __hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v.y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v.z = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          v.w = __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        const uint32_t cmd = __builtin_amdgcn_readlane(f, 1), off = __builtin_amdgcn_readlane(f, 2),
+                       len = __builtin_amdgcn_readlane(f, 3), inl = __builtin_amdgcn_readlane(f, 11);
+        if (cmd == 0u && inl) {
+          // the inline span: its staging bytes [0, off + len) sit at the inline
+          // area's start (64-byte aligned, so address parity is the staging's)
+          uint32_t acc = 0;
+          if (lane >= 16 && lane < 32) acc = range_sum(v, (int)(16u * (lane - 16u)) - (int)off, 0, (int)len);
+          acc = group_sum<64>(acc);
+          if (lane == 0) {
+            const uint32_t abs_lanes = __builtin_amdgcn_readlane(f, 4), pseudo = __builtin_amdgcn_readlane(f, 5);
+            uint64_t sum = fold16_64(acc);
+            if (!abs_lanes && (off & 1u)) sum = swap16((uint32_t)sum);
+            if (pseudo)
+              sum += (uint64_t)__builtin_amdgcn_readlane(f, 6) + __builtin_amdgcn_readlane(f, 7) +
+                     (__builtin_amdgcn_readlane(f, 8) << 8) + swap16(__builtin_amdgcn_readlane(f, 9) & 0xffffu);
+            const uint32_t res = ~fold16_64(sum) & 0xffffu;
+            scalar_result(out, sq, res, __builtin_amdgcn_readlane(f, 10) != 0u, t_seen);
+          }
+          served = 1;
+        }
+        if (lane >= 1 && lane < 12) req[lane] = f;
       }
-      if (threadIdx.x == 0) req[0] = sq;
+      if (lane == 0) {
+        req[0] = sq;
+        req[12] = served;
+      }
     }
     __syncthreads();
     const uint32_t sq = req[0];
     if (sq == last || req[1] != 0u) break;  // idle, or a stop request
-    const uint64_t t_seen = rt_clock();
-    // every wave: the staging bytes are ordinary page-locked memory the host
-    // rewrote since the last request -- no cached copy of them may be used
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    const uint32_t res = scalar_span(base, bytes, req[2], req[3], req[4], req[5], req[6], req[7], req[8], req[9], part);
-    if (threadIdx.x == 0) {
-      if (req[10]) {
-        __hip_atomic_store((uint64_t *)(out + 2), t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store((uint64_t *)(out + 4), rt_clock(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      __hip_atomic_store(out, ((sq & 0xffffu) << 16) | res, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!req[12]) {
+      // every wave: the staging bytes are ordinary page-locked memory the host
+      // rewrote since the last request -- no cached copy of them may be used
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      const uint32_t res = scalar_span(base, bytes, req[2], req[3], req[4], req[5], req[6], req[7], req[8], req[9], part);
+      if (threadIdx.x == 0) scalar_result(out, sq, res, req[10] != 0u, t_seen);
     }
     last = sq;
     t_last = rt_clock();
     __syncthreads();  // req[] and part[] are rewritten by the next request
   }
 }
-
 
 namespace {
 
@@ -2156,6 +2199,11 @@ struct AqlDevice {
   hsa_agent_t agent{};
   double ns_per_tick = 1.0;
   AqlKernel k[kAqlKernels];
+  // the drop-in service's mailboxes: fine-grained device memory the host
+  // writes through the PCIe BAR (mbox_tried / mbox_ok: found once)
+  bool mbox_tried = false, mbox_ok = false;
+  hsa_amd_memory_pool_t mbox_pool{};
+  hsa_agent_t cpu{};
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -2631,9 +2679,13 @@ struct AqlOne {
   std::atomic<int> *err = nullptr;
   int error() const { return err ? err->load() : 0; }
   // the drop-in service (mi_aql_dropin_svc) running on this queue, and its
-  // mailbox (coherent page-locked host memory, ThreadCtx::sout + 16 words)
+  // mailbox: fine-grained device memory the host writes through the BAR
+  // (mbox_dev), else coherent page-locked host memory (ThreadCtx::sout + 16
+  // words).  The host never reads it back: mbox_seq shadows its sequence word.
   bool svc_live = false;
-  uint32_t *svc_box = nullptr;
+  uint32_t *mbox = nullptr;
+  bool mbox_dev = false;
+  uint32_t mbox_seq = 0;
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
@@ -2678,11 +2730,19 @@ int aql_one_wait(AqlOne &o) {
 }
 // Stop the thread's drop-in service and wait for its dispatch to retire: a
 // stop request (cmd 1) under a sequence word no tag can equal (bit 16 set).
+// Post a request: fields (and inline bytes) first, the sequence word last; a
+// device mailbox is write-combined BAR memory, hence the store fences.
+void mbox_post(AqlOne &o, uint32_t seq) {
+  if (o.mbox_dev) _mm_sfence();
+  __atomic_store_n(&o.mbox[0], seq, __ATOMIC_RELEASE);
+  if (o.mbox_dev) _mm_sfence();
+  o.mbox_seq = seq;
+}
 int svc_stop(AqlOne &o) {
   if (!o.svc_live) return 0;
-  volatile uint32_t *bx = o.svc_box;
+  volatile uint32_t *bx = o.mbox;
   bx[1] = 1u;
-  __atomic_store_n(&o.svc_box[0], (bx[0] + 0x10000u) | 0x10000u, __ATOMIC_RELEASE);
+  mbox_post(o, (o.mbox_seq + 0x10000u) | 0x10000u);
   int rc = aql_one_wait(o);
   if (rc) return rc;
   o.svc_live = false;
@@ -2726,6 +2786,7 @@ bool aql_one_release(AqlOne &o) {
       aql_queue_destroy(o.q);
       if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
       if (o.karg) (void)hipHostFree(o.karg);
+      if (o.mbox && o.mbox_dev) (void)hsa_amd_memory_pool_free(o.mbox);
       delete o.err;
     } else {
       leaked = true;
@@ -2746,7 +2807,9 @@ bool aql_one_release(AqlOne &o) {
   o.unretired = false;
   o.err = nullptr;
   o.svc_live = false;
-  o.svc_box = nullptr;
+  o.mbox = nullptr;
+  o.mbox_dev = false;
+  o.mbox_seq = 0;
   return leaked;
 }
 
@@ -2784,13 +2847,64 @@ void thread_exit_register() {
 // dispatch the completion signal without waiting (the drop-in service, whose
 // retirement the caller watches).  A running drop-in service is stopped first:
 // the packet behind it would wait for it (barrier bit).
-int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait,
-                   bool signal = false) {
-  AqlOne &o = t_aql1;
-  if (o.svc_live) {
-    int rc = svc_stop(o);
-    if (rc) return rc;
+// A drop-in service mailbox in the GPU's fine-grained device memory that the
+// CPU may write (through the PCIe BAR): the service then polls its own HBM
+// instead of host memory over PCIe.  nullptr when the platform does not map
+// device memory for the CPU (or MI_CKSUM_DROPIN_MAILBOX=host): the mailbox is
+// then page-locked host memory.
+hsa_status_t mbox_cpu_cb(hsa_agent_t a, void *data) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *(hsa_agent_t *)data = a;
+    return HSA_STATUS_INFO_BREAK;
   }
+  return HSA_STATUS_SUCCESS;
+}
+hsa_status_t mbox_pool_cb(hsa_amd_memory_pool_t pool, void *data) {
+  AqlDevice *a = (AqlDevice *)data;
+  hsa_amd_segment_t seg;
+  uint32_t flags = 0;
+  bool alloc = false;
+  hsa_amd_memory_pool_access_t acc = HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED;
+  if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL ||
+      hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS ||
+      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) ||
+      hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc) != HSA_STATUS_SUCCESS ||
+      !alloc ||
+      hsa_amd_agent_memory_pool_get_info(a->cpu, pool, HSA_AMD_AGENT_MEMORY_POOL_INFO_ACCESS, &acc) !=
+          HSA_STATUS_SUCCESS ||
+      acc == HSA_AMD_MEMORY_POOL_ACCESS_NEVER_ALLOWED)
+    return HSA_STATUS_SUCCESS;
+  a->mbox_pool = pool;
+  a->mbox_ok = true;
+  return HSA_STATUS_INFO_BREAK;
+}
+uint32_t *mbox_alloc(AqlDevice *a) {
+  {
+    std::lock_guard<std::mutex> lk(g_aql_mu);
+    if (!a->mbox_tried) {
+      a->mbox_tried = true;
+      const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
+      if (!(e && !strcmp(e, "host")) && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK)
+        (void)hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a);
+    }
+    if (!a->mbox_ok) return nullptr;
+  }
+  void *p = nullptr;
+  if (hsa_amd_memory_pool_allocate(a->mbox_pool, 4096, 0, &p) != HSA_STATUS_SUCCESS || !p) return nullptr;
+  if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+    (void)hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  volatile uint32_t *w = (volatile uint32_t *)p;
+  for (uint32_t k = 0; k < kSvcWords; ++k) w[k] = 0u;
+  _mm_sfence();
+  return (uint32_t *)p;
+}
+
+// The thread's queue on its current device (created on first use).
+int aql_one_open(AqlOne &o) {
   if (o.device != t_ctx.device) {
     if (aql_one_release(o)) return set_err(-EIO, "AQL engine: the thread's previous queue never retired");
     int rc = aql_device(t_ctx.device, &o.dev);
@@ -2810,6 +2924,17 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
     o.device = t_ctx.device;
     thread_exit_register();
   }
+  return 0;
+}
+int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait,
+                   bool signal = false) {
+  AqlOne &o = t_aql1;
+  if (o.svc_live) {
+    int rc = svc_stop(o);
+    if (rc) return rc;
+  }
+  int rc = aql_one_open(o);
+  if (rc) return rc;
   const AqlKernel &k = o.dev->k[id];
   if (k.kernarg > 512u) return set_err(-EPROTO, "AQL engine: kernarg segment %u B", k.kernarg);
   uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
@@ -2819,8 +2944,7 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   aql_fill_packet(t, k, blocks, ka, wg);
   uint64_t idx;
   void *p;
-  int rc = aql_one_slot(o, &idx, &p);
-  if (rc) return rc;
+  if ((rc = aql_one_slot(o, &idx, &p))) return rc;
   hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)p;
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
   const bool sig = wait || signal;
@@ -4087,10 +4211,11 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     return set_err(-EINVAL, "scalar staging overrun");
   if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
   if (!c.sout) {
-    // words 0..5: the result and the trace stamps; 16..26: the service mailbox
-    HIP_TRY(hipHostMalloc((void **)&c.sout, 128, hipHostMallocMapped | hipHostMallocCoherent));
+    // words 0..5: the result and the trace stamps; 16..: the service mailbox
+    // when it lives in host memory
+    HIP_TRY(hipHostMalloc((void **)&c.sout, 512, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
-    memset(c.sout, 0, 128);
+    memset(c.sout, 0, 512);
   }
   c.stag = (c.stag + 1) & 0xffffu;
   const uint32_t tag = c.stag;
@@ -4123,17 +4248,24 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   uint32_t prev = 0;
   // (re)start the service: it serves any sequence word other than seq0
   auto svc_launch = [&](uint32_t seq0) -> int {
-    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, 0u, c.sout_dev + 16, c.sout_dev, seq0,
-                    dropin_svc_idle_ticks()};
+    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, 0u,
+                    o.mbox_dev ? o.mbox : c.sout_dev + 16, c.sout_dev, seq0, dropin_svc_idle_ticks()};
     int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
     if (r) return r;
-    o.svc_box = c.sout + 16;
     o.svc_live = true;
     return 0;
   };
   if (svc) {
-    volatile uint32_t *bx = c.sout + 16;
-    prev = bx[0];
+    if ((rc = aql_one_open(o))) return rc;
+    if (!o.mbox) {
+      uint32_t *m = mbox_alloc(o.dev);
+      o.mbox_dev = m != nullptr;
+      o.mbox = m ? m : c.sout + 16;
+      o.mbox_seq = 0;
+    }
+    volatile uint32_t *bx = o.mbox;
+    prev = o.mbox_seq;
+    const bool inl = off + len <= kSvcInlineBytes;
     bx[1] = 0u;  // cmd: fold
     bx[2] = (uint32_t)off;
     bx[3] = len;
@@ -4144,8 +4276,15 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     bx[8] = proto;
     bx[9] = plen;
     bx[10] = trace ? 1u : 0u;
+    bx[11] = inl ? 1u : 0u;
+    if (inl) {
+      // the staging bytes [0, off + len) into the mailbox's inline area
+      const uint32_t nw = (uint32_t)(off + len + 3u) >> 2;
+      const uint32_t *sw = (const uint32_t *)c.stage;
+      for (uint32_t k = 0; k < nw; ++k) bx[kSvcInline + k] = sw[k];
+    }
     if (!o.svc_live && (rc = svc_launch(prev))) return rc;
-    __atomic_store_n(&c.sout[16], tag, __ATOMIC_RELEASE);
+    mbox_post(o, tag);
     if (trace) t_dtrace.t_doorbell = sys_ts();
   } else if (aql) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
@@ -4251,6 +4390,9 @@ int mi__set_dropin_service(int on) {
 }
 // Is the calling thread's drop-in service running?  (tests)
 int mi__dropin_service_live(void) { return t_aql1.svc_live ? 1 : 0; }
+// Where the calling thread's service mailbox lives: 0 none yet, 1 page-locked
+// host memory, 2 device memory written through the BAR.  (tests, bench)
+int mi__dropin_mailbox(void) { return !t_aql1.mbox ? 0 : t_aql1.mbox_dev ? 2 : 1; }
 
 void mi__fatal(const char *what) {
   fprintf(stderr, "libmicksum: %s: %s\n", what, t_err[0] ? t_err : "unknown error");

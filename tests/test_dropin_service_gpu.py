@@ -57,6 +57,25 @@ def test_service_runs_and_answers(lib):
     assert mi.in_cksum_skip(m, 1480, 20) == _skip_want(1500, 20)
 
 
+def test_service_inline_and_staged_spans(lib):
+    """Spans up to 256 staging bytes travel inline in the mailbox and are
+    folded by wave 0; longer ones stay in the staging buffer: both sides of
+    the cut, odd lengths and starts, skips, pseudo headers, odd chains."""
+    lib.mi__dropin_mailbox.restype = C.c_int
+    rnd = random.Random(11)
+    for n in list(range(1, 40)) + [200, 236, 237, 250, 251, 255, 256, 257, 300, 511, 1500]:
+        k = rnd.randrange(0, 4)
+        segs = [(PAT[7:7 + n // 3], 1), (PAT[100:100 + n - n // 3 - k], 3), (PAT[900:900 + k], 2)]
+        m = mi.MbufChain(segs)
+        for skip in (0, 1, min(3, n)):
+            got = mi.in_cksum_skip(m, n - skip, skip)
+            assert got == ORC.chain_skip(segs, n - skip, skip), (n, skip)
+        got = mi.in_cksum_pseudo_header(m, n, 0, 0x0101A8C0, 0x0201A8C0, 17)
+        assert got == ORC.chain_pseudo(segs, n, 0, 0x0101A8C0, 0x0201A8C0, 17), n
+    assert lib.mi__dropin_mailbox() in (1, 2)
+    print("drop-in service mailbox:", {1: "host memory", 2: "device memory (BAR)"}[lib.mi__dropin_mailbox()])
+
+
 def test_service_idle_exit_and_relaunch(lib):
     """Calls spaced around the 1 ms idle exit: some find the service gone and
     launch another, some post just as it leaves; all answers right."""

@@ -37,6 +37,7 @@ def main():
     lib = mi.load()
     lib.mi__dropin_trace.argtypes = [C.c_int]
     lib.mi__dropin_trace_read.argtypes = [C.POINTER(C.c_double), C.c_int]
+    lib.mi__dropin_mailbox.restype = C.c_int
     lib.mi__set_dropin_service.restype = C.c_int
     lib.mi__set_dropin_service.argtypes = [C.c_int]
     pat = bytes(i & 0xFF for i in range(65536))
@@ -75,7 +76,8 @@ def main():
         r = np.array(rows)
         med = lambda x: round(float(np.median(x)), 3)  # noqa: E731
         print(json.dumps(dict(
-            call=name, mode=mode, calls=a.calls, untraced_call_us=med(np.array(plain) * 1e6),
+            call=name, mode=mode, calls=a.calls,
+            mailbox={0: None, 1: "host", 2: "device"}[lib.mi__dropin_mailbox()] if mode == "service" else None, untraced_call_us=med(np.array(plain) * 1e6),
             traced_call_us=med(np.array(tot) * 1e6),
             entry_to_posted_us=med(r[:, 0]),
             posted_to_result_seen_us=med(r[:, 2] - r[:, 0]),
