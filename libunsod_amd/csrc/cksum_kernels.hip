@@ -1461,25 +1461,27 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
 // resident while its thread keeps calling drop-ins, so a call costs no queue
 // dispatch.  The host writes the request into a mailbox -- fine-grained
 // device memory written through the PCIe BAR when the platform maps it for the
-// CPU, else coherent page-locked host memory: box[1..11] = cmd, off, len,
-// abs_lanes, pseudo, src, dst, proto, plen, trace, inline; a span of at most
-// kSvcInlineBytes bytes (with its staging offset) at box[kSvcInline..], else
+// CPU, else coherent page-locked host memory: box[2..10] = off, len,
+// abs_lanes, pseudo, src, dst, proto, plen, trace; a span of at most
+// kSvcInlineBytes staging bytes (offset included) at box[kSvcInline..], else
 // the span stays in the page-locked staging buffer; then box[0], the request's
-// sequence word, last.  Lane 0 polls box[0]; once it moves, ONE round trip
-// brings the fields (lanes 1..11) and the inline span (lanes 16..31), and an
-// inline span is folded by wave 0 alone; a staged one by the whole workgroup
-// (scalar_span).  The result goes to the caller's pinned word as mi_aql_scalar
-// stores it.  Exit conditions every wave reaches: a stop request (cmd 1), or
-// no new request for idle_ticks of the 100 MHz clock -- the host sees the
+// sequence word, last: the call's 16-bit tag, the inline span's 16-byte chunk
+// count in bits 16..23, bit 31 for a stop request.  Lane 0 polls box[0]; once
+// it moves, ONE round trip brings the fields (lanes 2..10) and the inline
+// chunks (two per lane at most), and an inline span is folded by wave 0 alone;
+// a staged one by the whole workgroup (scalar_span).  The result goes to the
+// caller's pinned word as mi_aql_scalar stores it.  Exit conditions every wave
+// reaches: a stop request, or no new request for idle_ticks of the 100 MHz
+// clock -- the host sees the
 // dispatch retire (its completion signal) and launches a new one when the next
 // call comes.  With trace set, out[2..5] get the clock at the moment the
 // request was seen and at the result store.
-constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 256, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
+constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 2048, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
                                                                              const uint32_t *box, uint32_t *out,
                                                                              uint32_t seq0, uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
-  __shared__ uint32_t req[13];  // [0] sequence, [1..11] fields, [12] served by wave 0
+  __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [12] served by wave 0
   uint32_t last = seq0;
   uint64_t t_last = rt_clock(), t_seen = 0;
   for (;;) {
@@ -1498,37 +1500,45 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
       if (sq != last) {
         t_seen = rt_clock();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t nck = (sq >> 16) & 0xffu;
         uint32_t f = 0;
-        u32x4 v{0, 0, 0, 0};
-        if (lane >= 1 && lane < 12) f = __hip_atomic_load(box + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (lane >= 16 && lane < 32) {
-          const uint32_t *q = box + kSvcInline + 4u * (lane - 16u);
-          v.x = __hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          v.y = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          v.z = __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          v.w = __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
+        auto ld4 = [&](uint32_t c) {
+          const uint32_t *q = box + kSvcInline + 4u * c;
+          return u32x4{__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                       __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)};
+        };
+        if (lane >= 2 && lane < 11) f = __hip_atomic_load(box + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (!(sq >> 31)) {
+          if (lane < nck) v0 = ld4(lane);
+          if (64u + lane < nck) v1 = ld4(64u + lane);
         }
-        const uint32_t cmd = __builtin_amdgcn_readlane(f, 1), off = __builtin_amdgcn_readlane(f, 2),
-                       len = __builtin_amdgcn_readlane(f, 3), inl = __builtin_amdgcn_readlane(f, 11);
-        if (cmd == 0u && inl) {
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane(f, 2), len = (uint32_t)__builtin_amdgcn_readlane(f, 3);
+        if (!(sq >> 31) && nck) {
           // the inline span: its staging bytes [0, off + len) sit at the inline
           // area's start (64-byte aligned, so address parity is the staging's)
-          uint32_t acc = 0;
-          if (lane >= 16 && lane < 32) acc = range_sum(v, (int)(16u * (lane - 16u)) - (int)off, 0, (int)len);
+          uint32_t acc = range_sum(v0, (int)(16u * lane) - (int)off, 0, (int)len) +
+                         range_sum(v1, (int)(16u * (64u + lane)) - (int)off, 0, (int)len);
           acc = group_sum<64>(acc);
           if (lane == 0) {
-            const uint32_t abs_lanes = __builtin_amdgcn_readlane(f, 4), pseudo = __builtin_amdgcn_readlane(f, 5);
+            const uint32_t abs_lanes = (uint32_t)__builtin_amdgcn_readlane(f, 4),
+                           pseudo = (uint32_t)__builtin_amdgcn_readlane(f, 5);
             uint64_t sum = fold16_64(acc);
             if (!abs_lanes && (off & 1u)) sum = swap16((uint32_t)sum);
-            if (pseudo)
-              sum += (uint64_t)__builtin_amdgcn_readlane(f, 6) + __builtin_amdgcn_readlane(f, 7) +
-                     (__builtin_amdgcn_readlane(f, 8) << 8) + swap16(__builtin_amdgcn_readlane(f, 9) & 0xffffu);
+            // (readlane returns int: through uint32_t, or a source address
+            // above 2^31 would be sign-extended into the 64-bit sum)
+            const uint32_t src = (uint32_t)__builtin_amdgcn_readlane(f, 6), dst = (uint32_t)__builtin_amdgcn_readlane(f, 7),
+                           proto = (uint32_t)__builtin_amdgcn_readlane(f, 8),
+                           plen = (uint32_t)__builtin_amdgcn_readlane(f, 9);
+            if (pseudo) sum += (uint64_t)src + dst + (proto << 8) + swap16(plen & 0xffffu);
             const uint32_t res = ~fold16_64(sum) & 0xffffu;
             scalar_result(out, sq, res, __builtin_amdgcn_readlane(f, 10) != 0u, t_seen);
           }
           served = 1;
         }
-        if (lane >= 1 && lane < 12) req[lane] = f;
+        if (lane >= 2 && lane < 11) req[lane] = f;
       }
       if (lane == 0) {
         req[0] = sq;
@@ -1537,7 +1547,7 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
     }
     __syncthreads();
     const uint32_t sq = req[0];
-    if (sq == last || req[1] != 0u) break;  // idle, or a stop request
+    if (sq == last || (sq >> 31)) break;  // idle, or a stop request
     if (!req[12]) {
       // every wave: the staging bytes are ordinary page-locked memory the host
       // rewrote since the last request -- no cached copy of them may be used
@@ -2740,9 +2750,7 @@ void mbox_post(AqlOne &o, uint32_t seq) {
 }
 int svc_stop(AqlOne &o) {
   if (!o.svc_live) return 0;
-  volatile uint32_t *bx = o.mbox;
-  bx[1] = 1u;
-  mbox_post(o, (o.mbox_seq + 0x10000u) | 0x10000u);
+  mbox_post(o, 0x80000000u | ((o.mbox_seq + 1u) & 0xffffu));  // bit 31: stop
   int rc = aql_one_wait(o);
   if (rc) return rc;
   o.svc_live = false;
@@ -2849,7 +2857,10 @@ void thread_exit_register() {
 // the packet behind it would wait for it (barrier bit).
 // A drop-in service mailbox in the GPU's fine-grained device memory that the
 // CPU may write (through the PCIe BAR): the service then polls its own HBM
-// instead of host memory over PCIe.  nullptr when the platform does not map
+// instead of host memory over PCIe.  (On the MI355X boxes the plain
+// fine-grained VRAM pool is never CPU-accessible; the extended-scope
+// fine-grained one is, once allowed: tools/pool_probe.cpp,
+// profiles/r04/pool_probe_r04.jsonl.)  nullptr when the platform does not map
 // device memory for the CPU (or MI_CKSUM_DROPIN_MAILBOX=host): the mailbox is
 // then page-locked host memory.
 hsa_status_t mbox_cpu_cb(hsa_agent_t a, void *data) {
@@ -2869,7 +2880,8 @@ hsa_status_t mbox_pool_cb(hsa_amd_memory_pool_t pool, void *data) {
   if (hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
       seg != HSA_AMD_SEGMENT_GLOBAL ||
       hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags) != HSA_STATUS_SUCCESS ||
-      !(flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) ||
+      !(flags & (HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED |
+                 HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_EXTENDED_SCOPE_FINE_GRAINED)) ||
       hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc) != HSA_STATUS_SUCCESS ||
       !alloc ||
       hsa_amd_agent_memory_pool_get_info(a->cpu, pool, HSA_AMD_AGENT_MEMORY_POOL_INFO_ACCESS, &acc) !=
@@ -4213,9 +4225,9 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   if (!c.sout) {
     // words 0..5: the result and the trace stamps; 16..: the service mailbox
     // when it lives in host memory
-    HIP_TRY(hipHostMalloc((void **)&c.sout, 512, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(hipHostMalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
-    memset(c.sout, 0, 512);
+    memset(c.sout, 0, 4096);
   }
   c.stag = (c.stag + 1) & 0xffffu;
   const uint32_t tag = c.stag;
@@ -4266,7 +4278,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     volatile uint32_t *bx = o.mbox;
     prev = o.mbox_seq;
     const bool inl = off + len <= kSvcInlineBytes;
-    bx[1] = 0u;  // cmd: fold
+    const uint32_t nck = inl ? (uint32_t)(off + len + 15u) >> 4 : 0u;
     bx[2] = (uint32_t)off;
     bx[3] = len;
     bx[4] = lanes == MI_SPAN_ABS ? 1u : 0u;
@@ -4276,15 +4288,11 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     bx[8] = proto;
     bx[9] = plen;
     bx[10] = trace ? 1u : 0u;
-    bx[11] = inl ? 1u : 0u;
-    if (inl) {
-      // the staging bytes [0, off + len) into the mailbox's inline area
-      const uint32_t nw = (uint32_t)(off + len + 3u) >> 2;
-      const uint32_t *sw = (const uint32_t *)c.stage;
-      for (uint32_t k = 0; k < nw; ++k) bx[kSvcInline + k] = sw[k];
-    }
+    // the staging bytes [0, off + len) into the mailbox's inline area, whole
+    // 16-byte chunks (the staging buffer holds at least 4 KiB)
+    if (nck) memcpy((void *)(bx + kSvcInline), c.stage, 16u * nck);
     if (!o.svc_live && (rc = svc_launch(prev))) return rc;
-    mbox_post(o, tag);
+    mbox_post(o, tag | (nck << 16));
     if (trace) t_dtrace.t_doorbell = sys_ts();
   } else if (aql) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,

@@ -58,12 +58,12 @@ def test_service_runs_and_answers(lib):
 
 
 def test_service_inline_and_staged_spans(lib):
-    """Spans up to 256 staging bytes travel inline in the mailbox and are
+    """Spans up to 2048 staging bytes travel inline in the mailbox and are
     folded by wave 0; longer ones stay in the staging buffer: both sides of
     the cut, odd lengths and starts, skips, pseudo headers, odd chains."""
     lib.mi__dropin_mailbox.restype = C.c_int
     rnd = random.Random(11)
-    for n in list(range(1, 40)) + [200, 236, 237, 250, 251, 255, 256, 257, 300, 511, 1500]:
+    for n in list(range(1, 40)) + [200, 255, 256, 257, 511, 1500, 2000, 2044, 2045, 2047, 2048, 2049, 2100, 4000]:
         k = rnd.randrange(0, 4)
         segs = [(PAT[7:7 + n // 3], 1), (PAT[100:100 + n - n // 3 - k], 3), (PAT[900:900 + k], 2)]
         m = mi.MbufChain(segs)

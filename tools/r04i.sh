@@ -9,4 +9,6 @@ tail -1 $O/gpu_tests_dropin.log
 timeout -k 10 180 python -u tools/dropin_breakdown.py --calls 400 > $O/dropin_breakdown.jsonl 2> $O/dropin.err || { tail $O/dropin.err; exit 1; }
 MI_CKSUM_DROPIN_MAILBOX=host timeout -k 10 180 python -u tools/dropin_breakdown.py --calls 400 > $O/dropin_breakdown_hostbox.jsonl 2>> $O/dropin.err || { tail $O/dropin.err; exit 1; }
 cut -c1-330 $O/dropin_breakdown.jsonl $O/dropin_breakdown_hostbox.jsonl
+./tools/pool_probe > $O/pool_probe.jsonl 2>&1 || true
+cat $O/pool_probe.jsonl
 echo done
