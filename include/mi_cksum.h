@@ -11,11 +11,15 @@
  *       signatures -- they replace the MACHINE_SRCS object in_cksum.o inside
  *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  Each call
  *       gathers the mbuf chain into a per-thread pinned staging buffer and
- *       writes one AQL dispatch packet into a per-thread HSA queue of the
- *       library's, then spins on a pinned result word: ~8-11 us per call on the
- *       MI355X host.  This level is the compatibility path (the
- *       reference's call sites unchanged); per-packet RX/TX throughput comes
- *       from (b2) at the burst / inject-ring batch points.
+ *       posts it to the thread's drop-in service -- one resident workgroup
+ *       polling a mailbox in device memory the host writes through the PCIe BAR
+ *       (spans up to 2 KiB travel in the mailbox itself) -- then spins on a
+ *       pinned result word: in_cksum_hdr ~2.9 us, a 1480-byte
+ *       in_cksum_pseudo_header ~3.7 us per call on the MI355X host (DESIGN.md
+ *       1; MI_CKSUM_DROPIN_SERVICE=0: one AQL dispatch per call, ~8 us).  This
+ *       level is the compatibility path (the reference's call sites unchanged);
+ *       per-packet RX/TX throughput comes from (b2) at the burst / inject-ring
+ *       batch points.
  *
  *  (b2) batch offload: a batch of packets that already sits in device memory
  *       (the RX burst / TX inject-ring batch points, uinet_if_dpdk.c:854-879 and

@@ -6,7 +6,8 @@
  * (src/sys/amd64/amd64/in_cksum.c:193-232 and :241-276: leading skip, zero-length
  * mbufs ignored, a short chain truncates silently), packs the selected bytes
  * contiguously into the thread's page-locked staging buffer and has the GPU fold
- * them (mi__scalar_fold, one launch + sync).  Packing preserves the checksum:
+ * them (mi__scalar_fold: a request to the thread's resident drop-in service,
+ * or one AQL dispatch, and a spin on the result).  Packing preserves the checksum:
  * the reference's (clen ^ addr) & 1 swap makes every span's lanes relative to
  * the stream, and a contiguous copy starting at an even address is exactly the
  * stream.  in_cksum_hdr keeps its address mod 16 in staging because its lanes
