@@ -1475,11 +1475,15 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
 // clock -- the host sees the
 // dispatch retire (its completion signal) and launches a new one when the next
 // call comes.  With trace set, out[2..5] get the clock at the moment the
-// request was seen and at the result store.
+// request was seen and at the result store.  On its way out the service
+// stores its launch token at out[6]: the process-exit handler waits for that
+// word (svc_atexit), so no service is still running when the runtime tears
+// the process's memory down.
 constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 2048, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
-                                                                             const uint32_t *box, uint32_t *out,
-                                                                             uint32_t seq0, uint32_t idle_ticks) {
+                                                                             uint32_t token, const uint32_t *box,
+                                                                             uint32_t *out, uint32_t seq0,
+                                                                             uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
   __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [12] served by wave 0
   uint32_t last = seq0;
@@ -1547,7 +1551,10 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
     }
     __syncthreads();
     const uint32_t sq = req[0];
-    if (sq == last || (sq >> 31)) break;  // idle, or a stop request
+    if (sq == last || (sq >> 31)) {  // idle, or a stop request
+      if (threadIdx.x == 0) __hip_atomic_store(out + 6, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
     if (!req[12]) {
       // every wave: the staging bytes are ordinary page-locked memory the host
       // rewrote since the last request -- no cached copy of them may be used
@@ -2696,6 +2703,9 @@ struct AqlOne {
   uint32_t *mbox = nullptr;
   bool mbox_dev = false;
   uint32_t mbox_seq = 0;
+  uint32_t svc_token = 0;              // the running service's launch token
+  volatile uint32_t *svc_out = nullptr;  // its result block (host): [6] = token on exit
+  bool svc_registered = false;         // in g_svc_reg (the process-exit handler's list)
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
@@ -2787,8 +2797,44 @@ int aql_one_quiesce(AqlOne &o) {
 // and result word that dispatch reads and writes -- are kept rather than
 // freed under a running kernel.  The reason is reported on stderr once per
 // leak and the queue moves from g_live_queues to g_leaked_queues.
+// Every thread's drop-in service, for the process-exit handler: a service
+// still polling when the runtime unmaps the process's memory at exit would
+// fault on its mailbox, so exit() first stops each one and waits (200 ms at
+// most) for it to store its token -- host memory only, no HSA call (the
+// runtime may be half torn down by then).  Registered on first launch (after
+// HIP's own exit handlers, so it runs before them).
+std::mutex g_svc_mu;
+std::vector<AqlOne *> g_svc_reg;
+std::atomic<uint32_t> g_svc_tokens{0};
+void svc_atexit() {
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  for (AqlOne *o : g_svc_reg) {
+    if (!o->svc_live || !o->svc_out || !o->mbox || o->svc_out[6] == o->svc_token) continue;
+    mbox_post(*o, 0x80000000u | ((o->mbox_seq + 1u) & 0xffffu));
+    const double t0 = mono_s();
+    while (o->svc_out[6] != o->svc_token && mono_s() - t0 < 0.2) {
+    }
+    o->svc_live = false;
+  }
+}
+void svc_register(AqlOne &o) {
+  if (o.svc_registered) return;
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  static const bool once = atexit(svc_atexit) == 0;
+  (void)once;
+  g_svc_reg.push_back(&o);
+  o.svc_registered = true;
+}
+void svc_unregister(AqlOne &o) {
+  if (!o.svc_registered) return;
+  std::lock_guard<std::mutex> lk(g_svc_mu);
+  g_svc_reg.erase(std::remove(g_svc_reg.begin(), g_svc_reg.end(), &o), g_svc_reg.end());
+  o.svc_registered = false;
+}
+
 bool aql_one_release(AqlOne &o) {
   bool leaked = false;
+  svc_unregister(o);
   if (o.q) {
     if (aql_one_quiesce(o) == 0) {
       aql_queue_destroy(o.q);
@@ -2818,6 +2864,7 @@ bool aql_one_release(AqlOne &o) {
   o.mbox = nullptr;
   o.mbox_dev = false;
   o.mbox_seq = 0;
+  o.svc_out = nullptr;
   return leaked;
 }
 
@@ -4246,7 +4293,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   static_assert(sizeof(ScalarArgs) == 56, "kernel-argument layout of mi_aql_scalar");
   struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
     const uint8_t *base;
-    uint32_t bytes, pad_;
+    uint32_t bytes, token;
     const uint32_t *box;
     uint32_t *out;
     uint32_t seq0, idle_ticks;
@@ -4263,10 +4310,14 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   uint32_t prev = 0;
   // (re)start the service: it serves any sequence word other than seq0
   auto svc_launch = [&](uint32_t seq0) -> int {
-    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, 0u,
+    const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
+    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, token,
                     o.mbox_dev ? o.mbox : c.sout_dev + 16, c.sout_dev, seq0, dropin_svc_idle_ticks()};
     int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
     if (r) return r;
+    o.svc_token = token;
+    o.svc_out = c.sout;
+    svc_register(o);
     o.svc_live = true;
     return 0;
   };

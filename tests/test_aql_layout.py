@@ -69,11 +69,11 @@ def test_aql_entry_points_kernarg_layout(tmp_path):
         for o, s, k in args:
             if k in HIDDEN:
                 assert o == SCALAR_EXPLICIT + HIDDEN[k], ("mi_aql_scalar", k, o)
-    # mi_aql_dropin_svc(base, bytes, box, out, seq0, idle_ticks): SvcArgs in
-    # mi__scalar_fold, 40 bytes
+    # mi_aql_dropin_svc(base, bytes, token, box, out, seq0, idle_ticks): SvcArgs
+    # in mi__scalar_fold, 40 bytes
     args, seg = ks["mi_aql_dropin_svc"]
     explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]
-    assert explicit == [(0, 8), (8, 4), (16, 8), (24, 8), (32, 4), (36, 4)], explicit
+    assert explicit == [(0, 8), (8, 4), (12, 4), (16, 8), (24, 8), (32, 4), (36, 4)], explicit
     if seg > 40:
         for o, s, k in args:
             if k in HIDDEN:

@@ -163,6 +163,27 @@ def test_service_thread_churn(lib):
     assert lib.mi__hsa_queues_leaked() == leaked0
 
 
+def test_process_exit_with_live_service():
+    """A process that exits right after its last drop-in (the service still
+    polling its mailbox) stops the service at exit -- the exit handler waits
+    for its token -- so nothing faults while the runtime tears the process
+    down; this process's GPU work is unaffected afterwards."""
+    import os
+    import subprocess
+    import sys
+    code = ("import libunsod_amd as mi, torch; torch.cuda.init()\n"
+            "h = bytes.fromhex('450000730000400040110000c0a80001c0a800c7')\n"
+            "assert all(mi.in_cksum_hdr(h, addr_mod=0) == 0x61B8 for _ in range(50))\n"
+            "print('ok')\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for _ in range(3):
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root)
+        assert r.returncode == 0 and r.stdout.strip() == "ok", (r.returncode, r.stderr[-2000:])
+    x = torch.arange(1 << 20, device="cuda", dtype=torch.int64)
+    assert int(x.sum().item()) == (1 << 20) * ((1 << 20) - 1) // 2
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("service", [0, 1])
 def test_breakdown_stamps(lib, service):
     """The breakdown's figures are consistent: request posted before the
