@@ -2234,7 +2234,17 @@ std::atomic<int> g_leaked_queues{0};
 // Every library-owned HSA queue reports its errors into the slot of the object
 // that owns it (an AqlRun or a thread's AqlOne), passed as the callback data:
 // one faulted queue fails that owner's later calls, not every handle's.
-void aql_queue_error(hsa_status_t st, hsa_queue_t *, void *slot) {
+// MI_CKSUM_DEBUG_QUEUES=1: every library queue's creation and error on stderr
+// (diagnostics: which queue a device-wide fault came from).
+bool debug_queues() {
+  static const bool on = [] {
+    const char *e = getenv("MI_CKSUM_DEBUG_QUEUES");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+void aql_queue_error(hsa_status_t st, hsa_queue_t *q, void *slot) {
+  if (debug_queues()) fprintf(stderr, "libmicksum: HSA queue %p error 0x%x\n", (void *)q, (unsigned)st);
   if (slot) static_cast<std::atomic<int> *>(slot)->store((int)st);
 }
 int aql_queue_create(hsa_agent_t agent, uint32_t size, std::atomic<int> *err, hsa_queue_t **q) {
@@ -2243,6 +2253,7 @@ int aql_queue_create(hsa_agent_t agent, uint32_t size, std::atomic<int> *err, hs
     *q = nullptr;
     return set_err(-EIO, "AQL engine: hsa_queue_create failed");
   }
+  if (debug_queues()) fprintf(stderr, "libmicksum: HSA queue %p created (size %u)\n", (void *)*q, size);
   g_live_queues.fetch_add(1);
   return 0;
 }
