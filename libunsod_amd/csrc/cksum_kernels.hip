@@ -2217,10 +2217,13 @@ struct AqlDevice {
   double ns_per_tick = 1.0;
   AqlKernel k[kAqlKernels];
   // the drop-in service's mailboxes: fine-grained device memory the host
-  // writes through the PCIe BAR (mbox_tried / mbox_ok: found once)
+  // writes through the PCIe BAR (mbox_tried / mbox_ok: found once), carved
+  // from one slab of kMboxSlots 4 KiB slots that is never freed
   bool mbox_tried = false, mbox_ok = false;
   hsa_amd_memory_pool_t mbox_pool{};
   hsa_agent_t cpu{};
+  uint8_t *mbox_slab = nullptr;
+  uint64_t mbox_used = 0;  // slot bitmap
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -2843,6 +2846,8 @@ void svc_unregister(AqlOne &o) {
   o.svc_registered = false;
 }
 
+void mbox_free(AqlDevice *a, uint32_t *m);
+
 bool aql_one_release(AqlOne &o) {
   bool leaked = false;
   svc_unregister(o);
@@ -2851,7 +2856,7 @@ bool aql_one_release(AqlOne &o) {
       aql_queue_destroy(o.q);
       if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
       if (o.karg) (void)hipHostFree(o.karg);
-      if (o.mbox && o.mbox_dev) (void)hsa_amd_memory_pool_free(o.mbox);
+      if (o.mbox && o.mbox_dev) mbox_free(o.dev, o.mbox);
       delete o.err;
     } else {
       leaked = true;
@@ -2915,12 +2920,18 @@ void thread_exit_register() {
 // the packet behind it would wait for it (barrier bit).
 // A drop-in service mailbox in the GPU's fine-grained device memory that the
 // CPU may write (through the PCIe BAR): the service then polls its own HBM
-// instead of host memory over PCIe.  (On the MI355X boxes the plain
-// fine-grained VRAM pool is never CPU-accessible; the extended-scope
-// fine-grained one is, once allowed: tools/pool_probe.cpp,
-// profiles/r04/pool_probe_r04.jsonl.)  nullptr when the platform does not map
-// device memory for the CPU (or MI_CKSUM_DROPIN_MAILBOX=host): the mailbox is
-// then page-locked host memory.
+// instead of host memory over PCIe (in_cksum_hdr 2.9 us per call against 5.0
+// with the host mailbox).  (On the MI355X boxes the plain fine-grained VRAM
+// pool is never CPU-accessible; the extended-scope fine-grained one is, once
+// allowed: tools/pool_probe.cpp, profiles/r04/pool_probe_r04.jsonl.)
+// OPT-IN (MI_CKSUM_DROPIN_MAILBOX=device): two whole-suite GPU runs with
+// per-thread device mailboxes allocated and freed ended in an illegal-address
+// fault reported by HIP several tests later, the same suite with host
+// mailboxes did not (profiles/r04/gpu_tests_*).  The cause is not isolated;
+// the mailboxes now come from one slab per device that is never freed
+// (threads return their slot), which removes the allocate/free churn of
+// CPU-mapped VRAM -- the remaining suspect.  nullptr (no device mailbox):
+// the mailbox is page-locked host memory.
 hsa_status_t mbox_cpu_cb(hsa_agent_t a, void *data) {
   hsa_device_type_t t;
   if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
@@ -2950,27 +2961,36 @@ hsa_status_t mbox_pool_cb(hsa_amd_memory_pool_t pool, void *data) {
   a->mbox_ok = true;
   return HSA_STATUS_INFO_BREAK;
 }
+constexpr uint32_t kMboxSlots = 64;
 uint32_t *mbox_alloc(AqlDevice *a) {
-  {
-    std::lock_guard<std::mutex> lk(g_aql_mu);
-    if (!a->mbox_tried) {
-      a->mbox_tried = true;
-      const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
-      if (!(e && !strcmp(e, "host")) && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK)
-        (void)hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a);
+  std::lock_guard<std::mutex> lk(g_aql_mu);
+  if (!a->mbox_tried) {
+    a->mbox_tried = true;
+    const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
+    void *p = nullptr;
+    if (e && !strcmp(e, "device") && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK &&
+        hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a) == HSA_STATUS_INFO_BREAK && a->mbox_ok &&
+        hsa_amd_memory_pool_allocate(a->mbox_pool, 4096u * kMboxSlots, 0, &p) == HSA_STATUS_SUCCESS && p) {
+      if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
+        a->mbox_slab = (uint8_t *)p;
+      } else {
+        (void)hsa_amd_memory_pool_free(p);
+      }
     }
-    if (!a->mbox_ok) return nullptr;
   }
-  void *p = nullptr;
-  if (hsa_amd_memory_pool_allocate(a->mbox_pool, 4096, 0, &p) != HSA_STATUS_SUCCESS || !p) return nullptr;
-  if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
-    (void)hsa_amd_memory_pool_free(p);
-    return nullptr;
-  }
-  volatile uint32_t *w = (volatile uint32_t *)p;
-  for (uint32_t k = 0; k < kSvcWords; ++k) w[k] = 0u;
+  if (!a->mbox_slab || !~a->mbox_used) return nullptr;
+  const uint32_t k = (uint32_t)__builtin_ctzll(~a->mbox_used);
+  a->mbox_used |= 1ull << k;
+  volatile uint32_t *w = (volatile uint32_t *)(a->mbox_slab + 4096u * k);
+  for (uint32_t j = 0; j < kSvcWords; ++j) w[j] = 0u;
   _mm_sfence();
-  return (uint32_t *)p;
+  return (uint32_t *)w;
+}
+// A thread's slot back to its device's slab (the slab itself is never freed).
+void mbox_free(AqlDevice *a, uint32_t *m) {
+  std::lock_guard<std::mutex> lk(g_aql_mu);
+  const uint64_t k = ((uint8_t *)m - a->mbox_slab) / 4096u;
+  if (a->mbox_slab && k < kMboxSlots) a->mbox_used &= ~(1ull << k);
 }
 
 // The thread's queue on its current device (created on first use).
@@ -4243,8 +4263,9 @@ uint8_t *mi__scalar_staging(size_t need) {
 // The drop-in service switch (on by default; MI_CKSUM_DROPIN_SERVICE=0 or
 // mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
 // (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
-// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_r04.jsonl):
-// in_cksum_hdr 2.9 us per call against 8.1 us for a dispatch per call.
+// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
+// in_cksum_hdr 5.0 us per call with the host mailbox (2.9 with the opt-in
+// device mailbox) against 8.1 us for a dispatch per call.
 std::atomic<int> g_dropin_svc{-1};
 bool dropin_svc_on() {
   int v = g_dropin_svc.load(std::memory_order_relaxed);

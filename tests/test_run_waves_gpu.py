@@ -41,8 +41,8 @@ def test_plan_names_the_workgroup(run_waves):
     buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
     offs = torch.arange(100, dtype=torch.int64, device="cuda") * 300
     lens = torch.full((100,), 280, dtype=torch.int32, device="cuda")
-    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == \
-        "k_ipv4_verify_packed<8,%d waves>" % run_waves
+    want = "k_ipv4_verify_packed<8>" if run_waves == 4 else "k_ipv4_verify_packed<8,%d waves>" % run_waves
+    assert mi.verify_plan(mi.PktBatch(buf, 100, offs=offs, lens=lens, packed=True)) == want
 
 
 def test_packed_golden(golden, run_waves):
