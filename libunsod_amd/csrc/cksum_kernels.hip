@@ -2924,14 +2924,14 @@ void thread_exit_register() {
 // with the host mailbox).  (On the MI355X boxes the plain fine-grained VRAM
 // pool is never CPU-accessible; the extended-scope fine-grained one is, once
 // allowed: tools/pool_probe.cpp, profiles/r04/pool_probe_r04.jsonl.)
-// OPT-IN (MI_CKSUM_DROPIN_MAILBOX=device): two whole-suite GPU runs with
-// per-thread device mailboxes allocated and freed ended in an illegal-address
-// fault reported by HIP several tests later, the same suite with host
-// mailboxes did not (profiles/r04/gpu_tests_*).  The cause is not isolated;
-// the mailboxes now come from one slab per device that is never freed
-// (threads return their slot), which removes the allocate/free churn of
-// CPU-mapped VRAM -- the remaining suspect.  nullptr (no device mailbox):
-// the mailbox is page-locked host memory.
+// Two whole-suite GPU runs with per-thread device mailboxes allocated and
+// freed ended in an illegal-address fault reported by HIP several tests
+// later, while the same suite with host mailboxes did not fault
+// (profiles/r04/gpu_tests_*): the mailboxes now come from one slab per device
+// that is never freed (threads return their slot), which removes the
+// allocate/free churn of CPU-mapped VRAM, and the whole suite ran green with
+// it.  MI_CKSUM_DROPIN_MAILBOX=host: page-locked host memory (also the
+// fallback, nullptr here, when the platform maps no VRAM for the CPU).
 hsa_status_t mbox_cpu_cb(hsa_agent_t a, void *data) {
   hsa_device_type_t t;
   if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
@@ -2968,7 +2968,7 @@ uint32_t *mbox_alloc(AqlDevice *a) {
     a->mbox_tried = true;
     const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
     void *p = nullptr;
-    if (e && !strcmp(e, "device") && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK &&
+    if (!(e && !strcmp(e, "host")) && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK &&
         hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a) == HSA_STATUS_INFO_BREAK && a->mbox_ok &&
         hsa_amd_memory_pool_allocate(a->mbox_pool, 4096u * kMboxSlots, 0, &p) == HSA_STATUS_SUCCESS && p) {
       if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
@@ -4264,8 +4264,8 @@ uint8_t *mi__scalar_staging(size_t need) {
 // mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
 // (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
 // host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
-// in_cksum_hdr 5.0 us per call with the host mailbox (2.9 with the opt-in
-// device mailbox) against 8.1 us for a dispatch per call.
+// in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
+// mailbox) against 8.1 us for a dispatch per call.
 std::atomic<int> g_dropin_svc{-1};
 bool dropin_svc_on() {
   int v = g_dropin_svc.load(std::memory_order_relaxed);
