@@ -513,8 +513,11 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
     verify_emit(pend, ip_out, l4_out, st_out, bad, d);
   }
 }
+#ifndef MI_RUN_MINW
+#define MI_RUN_MINW 1  // waves per SIMD the flat-run kernel is held to (register budget experiments)
+#endif
 template <int U, int MODE = 0, int NW = kBlock / 64>
-__global__ __launch_bounds__(64 * NW) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+__global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out,
                                                                 uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
                                                                 uint32_t abs_lanes) {
   packed_body<U, MODE, NW>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
