@@ -1483,12 +1483,43 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
 // word (svc_atexit), so no service is still running when the runtime tears
 // the process's memory down.
 constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 2048, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
+// A host-memory RX burst for the service (bit 30 of the sequence word): the
+// verify kernels' arguments (AqlArgs' layout), carried in the mailbox's inline
+// area; the descriptors follow them there.
+struct BurstArgs {
+  Desc d;
+  uint16_t *ip, *l4;
+  uint8_t *st;
+  uint32_t *bad;
+};
+constexpr uint32_t kSvcBurstMax = 128;  // datagrams (descriptors inline: 128 + 12 x 128 bytes)
+// The burst, one 16-lane group per datagram (verify_body's per-datagram work:
+// ip_input.c:459-471 + tcp_input.c:697-720 / the RX offload flags).
+__device__ __forceinline__ void svc_burst(const BurstArgs &a) {
+  constexpr int G = 16, U = 6;
+  const Desc &d = a.d;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  for (uint32_t i = threadIdx.x / G; i < d.n; i += kScalarThreads / G) {
+    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    u32x4 v[U];
+    issue_first<G, U>(r, off, flen, lane, v);
+    IpHdr ih;
+    bool hdr_ok, l4_ok;
+    uint32_t sum_h, sum_l;
+    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    if (lane == 0)
+      verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off), a.ip,
+                  a.l4, a.st, a.bad, d);
+  }
+}
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
                                                                              uint32_t token, const uint32_t *box,
                                                                              uint32_t *out, uint32_t seq0,
                                                                              uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
-  __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [12] served by wave 0
+  __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [11] a burst, [12] served by wave 0
+  __shared__ u32x4 s_args[8];   // a burst's BurstArgs
   uint32_t last = seq0;
   uint64_t t_last = rt_clock(), t_seen = 0;
   for (;;) {
@@ -1523,7 +1554,10 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
           if (64u + lane < nck) v1 = ld4(64u + lane);
         }
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane(f, 2), len = (uint32_t)__builtin_amdgcn_readlane(f, 3);
-        if (!(sq >> 31) && nck) {
+        const bool burst = !(sq >> 31) && ((sq >> 30) & 1u);
+        if (burst && lane < nck && lane < 8u) s_args[lane] = v0;
+        if (lane == 0) req[11] = burst ? 1u : 0u;
+        if (!(sq >> 31) && !burst && nck) {
           // the inline span: its staging bytes [0, off + len) sit at the inline
           // area's start (64-byte aligned, so address parity is the staging's)
           uint32_t acc = range_sum(v0, (int)(16u * lane) - (int)off, 0, (int)len) +
@@ -1558,7 +1592,17 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
       if (threadIdx.x == 0) __hip_atomic_store(out + 6, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
-    if (!req[12]) {
+    if (req[11]) {
+      // a host RX burst: every wave, then the result word once every wave's
+      // outputs are visible at system scope
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      BurstArgs a;
+      __builtin_memcpy(&a, (const void *)s_args, sizeof a);
+      svc_burst(a);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __syncthreads();
+      if (threadIdx.x == 0) scalar_result(out, sq, 0u, false, t_seen);
+    } else if (!req[12]) {
       // every wave: the staging bytes are ordinary page-locked memory the host
       // rewrote since the last request -- no cached copy of them may be used
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
@@ -2206,6 +2250,7 @@ struct AqlArgs {
   uint8_t *st;
   uint32_t *bad;
 };
+static_assert(sizeof(AqlArgs) == sizeof(BurstArgs) && sizeof(BurstArgs) <= 128, "a burst's arguments in 8 chunks");
 constexpr uint32_t kAqlHidden = (sizeof(AqlArgs) + 7u) & ~7u;
 
 struct AqlKernel {
@@ -3840,6 +3885,108 @@ int mi_cksum_host_unregister(void *p) {
   return 0;
 }
 
+// The drop-in service switch (on by default; MI_CKSUM_DROPIN_SERVICE=0 or
+// mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
+// (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
+// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
+// in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
+// mailbox) against 8.1 us for a dispatch per call.
+std::atomic<int> g_dropin_svc{-1};
+bool dropin_svc_on() {
+  int v = g_dropin_svc.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE");
+    v = e && e[0] == '0' ? 0 : 1;
+    g_dropin_svc.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+uint32_t dropin_svc_idle_ticks() {
+  static const uint32_t t = [] {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_IDLE_US");
+    const long us = e ? atol(e) : 0;
+    return (uint32_t)((us > 0 && us < 10000000 ? us : 1000) * 100);  // the 100 MHz clock
+  }();
+  return t;
+}
+
+// The service machinery shared by the (b1) drop-ins (mi__scalar_fold) and the
+// small host RX bursts (verify_host_zero_copy): the thread's queue, its
+// mailbox and result block, (re)launch, one request and its result word.
+struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
+  const uint8_t *base;
+  uint32_t bytes, token;
+  const uint32_t *box;
+  uint32_t *out;
+  uint32_t seq0, idle_ticks;
+};
+static_assert(sizeof(SvcArgs) == 40, "kernel-argument layout of mi_aql_dropin_svc");
+static int ensure_sout(ThreadCtx &c) {
+  if (c.sout) return 0;
+  // words 0..5: the result and the trace stamps; 16..: the service mailbox
+  // when it lives in host memory
+  HIP_TRY(hipHostMalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
+  memset(c.sout, 0, 4096);
+  return 0;
+}
+static int svc_open(ThreadCtx &c, AqlOne &o) {
+  int rc = ensure_sout(c);
+  if (rc || (rc = aql_one_open(o))) return rc;
+  if (!o.mbox) {
+    uint32_t *m = mbox_alloc(o.dev);
+    o.mbox_dev = m != nullptr;
+    o.mbox = m ? m : c.sout + 16;
+    o.mbox_seq = 0;
+  }
+  return 0;
+}
+// the mailbox as the GPU addresses it
+static uint32_t *svc_box_dev(ThreadCtx &c, AqlOne &o) { return o.mbox_dev ? o.mbox : c.sout_dev + 16; }
+// (re)start the service: it serves any sequence word other than seq0
+static int svc_launch(ThreadCtx &c, AqlOne &o, uint32_t seq0) {
+  const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
+  const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, token, svc_box_dev(c, o), c.sout_dev, seq0,
+                  dropin_svc_idle_ticks()};
+  int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
+  if (r) return r;
+  o.svc_token = token;
+  o.svc_out = c.sout;
+  svc_register(o);
+  o.svc_live = true;
+  return 0;
+}
+// Spin on the result word for `tag`; relaunch the service if it retired
+// (idle exit) before serving the request posted after `prev`.
+static int svc_wait(ThreadCtx &c, AqlOne &o, uint32_t tag, uint32_t prev, uint32_t *word) {
+  volatile uint32_t *slot = c.sout;
+  const double t0 = mono_s();
+  for (uint32_t polls = 1;; ++polls) {
+    uint32_t v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+    if ((v >> 16) == tag) {
+      *word = v;
+      return 0;
+    }
+    if ((polls & 255u) == 0) {
+      if (o.error()) return set_err(-EIO, "drop-in service: queue error 0x%x", o.error());
+      const bool retired = hsa_signal_load_scacquire(o.sig) == 0;
+      v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);  // (the store and the completion race)
+      if ((v >> 16) == tag) {
+        *word = v;
+        return 0;
+      }
+      if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "drop-in service: no result after 10 s");
+      if (retired) {
+        // the service took its idle exit before this request: a new one
+        o.svc_live = false;
+        o.unretired = false;
+        int rc = svc_launch(c, o, prev);
+        if (rc) return rc;
+      }
+    }
+  }
+}
+
 // Zero-copy host path: the batch was page-locked with mi_cksum_host_register
 // (mapped into the GPU's address space), so the verify kernel reads the
 // datagram bytes where the NIC left them, over PCIe, with no staging copy and
@@ -3926,7 +4073,47 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   int id = -1;
   unsigned blocks = 0;
   AqlDevice *adv = nullptr;
-  if (host_aql && aql_device(t_ctx.device, &adv) == 0 &&
+  // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default
+  // kSvcBurstMax; 0: never) go to the thread's drop-in service instead of a
+  // dispatch: the kernel arguments and the descriptors travel in its mailbox
+  // (VRAM, written through the BAR), one 16-lane group per datagram, and the
+  // service stores the result word once every output is visible.
+  static const uint32_t burst_max = [] {
+    const char *e = getenv("MI_CKSUM_BURST_SERVICE_MAX");
+    const long v = e ? atol(e) : (long)kSvcBurstMax;
+    return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
+  }();
+  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0) {
+    AqlOne &o = t_aql1;
+    int rc = svc_open(c, o);
+    if (rc) return rc;
+    uint8_t *inl = (uint8_t *)(o.mbox + kSvcInline);                  // host view
+    const uint8_t *inl_dev = (const uint8_t *)(svc_box_dev(c, o) + kSvcInline);  // the GPU's
+    BurstArgs a{};
+    a.d = d;
+    size_t at = 128;  // the arguments, then offsets and lengths
+    if (b->offs) {
+      const size_t ob = ((b->flags & MI_BATCH_OFFS32) ? 4u : 8u) * n;
+      memcpy(inl + at, b->offs, ob);
+      a.d.offs = (const uint64_t *)(inl_dev + at);
+      at += (ob + 15u) & ~15ull;
+    }
+    if (b->lens) {
+      memcpy(inl + at, b->lens, 4u * n);
+      a.d.lens = (const uint32_t *)(inl_dev + at);
+    }
+    a.ip = zip;
+    a.l4 = zl4;
+    a.st = zst;
+    a.bad = nullptr;
+    memcpy(inl, &a, sizeof a);
+    c.stag = (c.stag + 1) & 0xffffu;
+    const uint32_t tag = c.stag, prev = o.mbox_seq;
+    if (!o.svc_live && (rc = svc_launch(c, o, prev))) return rc;
+    mbox_post(o, 0x40000000u | (((uint32_t)(sizeof a + 15u) >> 4) << 16) | tag);  // bit 30: a burst
+    uint32_t w;
+    if ((rc = svc_wait(c, o, tag, prev, &w))) return rc;
+  } else if (host_aql && aql_device(t_ctx.device, &adv) == 0 &&
       (wide ? aql_kernel_for_shape(d, Shape{64, 4}, &id, &blocks)
                         : aql_kernel_for(d, max_len, &id, &blocks)) == 0) {
     const AqlArgs args{d, zip, zl4, zst, zbad};
@@ -4263,31 +4450,6 @@ uint8_t *mi__scalar_staging(size_t need) {
   return c.stage;
 }
 
-// The drop-in service switch (on by default; MI_CKSUM_DROPIN_SERVICE=0 or
-// mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
-// (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
-// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
-// in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
-// mailbox) against 8.1 us for a dispatch per call.
-std::atomic<int> g_dropin_svc{-1};
-bool dropin_svc_on() {
-  int v = g_dropin_svc.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE");
-    v = e && e[0] == '0' ? 0 : 1;
-    g_dropin_svc.store(v, std::memory_order_relaxed);
-  }
-  return v == 1;
-}
-uint32_t dropin_svc_idle_ticks() {
-  static const uint32_t t = [] {
-    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_IDLE_US");
-    const long us = e ? atol(e) : 0;
-    return (uint32_t)((us > 0 && us < 10000000 ? us : 1000) * 100);  // the 100 MHz clock
-  }();
-  return t;
-}
-
 // One (b1) fold.  The kernel stores (tag << 16) | sum into the pinned slot
 // with a system-scope store and the host spins on the slot (a few us sooner
 // than a completion signal).  Either one dispatch per call (mi_aql_scalar: an
@@ -4307,13 +4469,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   if (!c.stage || off + len > c.stage_cap || c.stage_cap > kMaxBytes)
     return set_err(-EINVAL, "scalar staging overrun");
   if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
-  if (!c.sout) {
-    // words 0..5: the result and the trace stamps; 16..: the service mailbox
-    // when it lives in host memory
-    HIP_TRY(hipHostMalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
-    HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
-    memset(c.sout, 0, 4096);
-  }
+  if ((rc = ensure_sout(c))) return rc;
   c.stag = (c.stag + 1) & 0xffffu;
   const uint32_t tag = c.stag;
   const bool trace = t_dtrace.on;
@@ -4326,14 +4482,6 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     uint32_t *out;
   };
   static_assert(sizeof(ScalarArgs) == 56, "kernel-argument layout of mi_aql_scalar");
-  struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
-    const uint8_t *base;
-    uint32_t bytes, token;
-    const uint32_t *box;
-    uint32_t *out;
-    uint32_t seq0, idle_ticks;
-  };
-  static_assert(sizeof(SvcArgs) == 40, "kernel-argument layout of mi_aql_dropin_svc");
   static const bool host_aql = [] {
     const char *e = getenv("MI_CKSUM_HOST_AQL");
     return !(e && e[0] == '0');
@@ -4343,27 +4491,8 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   const bool svc = aql && dropin_svc_on();
   AqlOne &o = t_aql1;
   uint32_t prev = 0;
-  // (re)start the service: it serves any sequence word other than seq0
-  auto svc_launch = [&](uint32_t seq0) -> int {
-    const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
-    const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, token,
-                    o.mbox_dev ? o.mbox : c.sout_dev + 16, c.sout_dev, seq0, dropin_svc_idle_ticks()};
-    int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
-    if (r) return r;
-    o.svc_token = token;
-    o.svc_out = c.sout;
-    svc_register(o);
-    o.svc_live = true;
-    return 0;
-  };
   if (svc) {
-    if ((rc = aql_one_open(o))) return rc;
-    if (!o.mbox) {
-      uint32_t *m = mbox_alloc(o.dev);
-      o.mbox_dev = m != nullptr;
-      o.mbox = m ? m : c.sout + 16;
-      o.mbox_seq = 0;
-    }
+    if ((rc = svc_open(c, o))) return rc;
     volatile uint32_t *bx = o.mbox;
     prev = o.mbox_seq;
     const bool inl = off + len <= kSvcInlineBytes;
@@ -4380,7 +4509,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     // the staging bytes [0, off + len) into the mailbox's inline area, whole
     // 16-byte chunks (the staging buffer holds at least 4 KiB)
     if (nck) memcpy((void *)(bx + kSvcInline), c.stage, 16u * nck);
-    if (!o.svc_live && (rc = svc_launch(prev))) return rc;
+    if (!o.svc_live && (rc = svc_launch(c, o, prev))) return rc;
     mbox_post(o, tag | (nck << 16));
     if (trace) t_dtrace.t_doorbell = sys_ts();
   } else if (aql) {
@@ -4401,32 +4530,28 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   volatile uint32_t *slot = c.sout;
   uint32_t v = 0;
   const double t0 = mono_s();
-  for (uint32_t polls = 1;; ++polls) {
-    v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-    if ((v >> 16) == tag) break;
-    if ((polls & 255u) == 0) {
-      // has the work ended without the word?  (re-read after: the store and
-      // the completion race)
-      bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
-      if (aql) {
-        if (o.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", o.error());
-        if (svc) retired = hsa_signal_load_scacquire(o.sig) == 0;
-      } else {
-        const hipError_t e = hipStreamQuery(c.sstream);
-        if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));
-        retired = e == hipSuccess;
-      }
+  if (svc) {
+    if ((rc = svc_wait(c, o, tag, prev, &v))) return rc;
+  } else {
+    for (uint32_t polls = 1;; ++polls) {
       v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
       if ((v >> 16) == tag) break;
-      if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "scalar fold: no result after 10 s");
-      if (retired && svc) {
-        // the service took its idle exit before this request: a new one
-        o.svc_live = false;
-        o.unretired = false;
-        if ((rc = svc_launch(prev))) return rc;
-        continue;
+      if ((polls & 255u) == 0) {
+        // has the work ended without the word?  (re-read after: the store and
+        // the completion race)
+        bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
+        if (aql) {
+          if (o.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", o.error());
+        } else {
+          const hipError_t e = hipStreamQuery(c.sstream);
+          if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));
+          retired = e == hipSuccess;
+        }
+        v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+        if ((v >> 16) == tag) break;
+        if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "scalar fold: no result after 10 s");
+        if (retired) return set_err(-EIO, "scalar fold: the kernel ended without a result");
       }
-      if (retired) return set_err(-EIO, "scalar fold: the kernel ended without a result");
     }
   }
   *out = (uint16_t)(v & 0xffffu);

@@ -202,3 +202,37 @@ def test_breakdown_stamps(lib, service):
     r = np.median(np.array(rows), axis=0)
     assert 0 <= r[0] <= r[2], r
     assert 0 < r[1] <= r[2] - r[0], r
+
+
+def test_small_host_bursts_through_the_service(lib, demux_golden):
+    """Host-memory bursts of at most 128 datagrams go to the thread's service
+    (arguments and descriptors in its mailbox), larger ones to a dispatch:
+    the reference-generated demux golden (TCP / UDP / ICMP / IGMP / CARP,
+    options, fragments, bad sums, malformed headers) in bursts of 1-128 must
+    give the golden ip / l4 / status and the same RX offload flags as one
+    720-datagram dispatch, with u64 and u32 offsets."""
+    from conftest import aligned
+    g = demux_golden
+    keep, buf = aligned(g["ver_in"].copy(), 4096)
+    offs, flen = g["offs"].astype(np.int64), g["flen"].astype(np.int32)
+    n = len(offs)
+    mi.host_register(buf)
+    try:
+        fl_all, cd_all, _ = mi.rx_offload_host(buf, n, offs=offs, lens=flen, demux=True)
+        assert lib.mi__dropin_service_live() == 0  # 720 > 128: a dispatch
+        for size in (1, 7, 32, 100, 128):
+            for offs32 in (False, True):
+                ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
+                fl = np.zeros(n, np.uint32); cd = np.zeros(n, np.uint32)
+                for i0 in range(0, n, size):
+                    i1 = min(n, i0 + size)
+                    ip[i0:i1], l4[i0:i1], st[i0:i1], _ = mi.ipv4_verify_host(
+                        buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1], demux=True, offs32=offs32)
+                    assert lib.mi__dropin_service_live() == 1
+                    fl[i0:i1], cd[i0:i1], _ = mi.rx_offload_host(buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1],
+                                                                demux=True, offs32=offs32)
+                assert np.array_equal(st, g["st"]), (size, offs32)
+                assert np.array_equal(ip, g["ip"]) and np.array_equal(l4, g["l4"]), (size, offs32)
+                assert np.array_equal(fl, fl_all) and np.array_equal(cd, cd_all), (size, offs32)
+    finally:
+        mi.host_unregister(buf)
