@@ -4073,14 +4073,18 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   int id = -1;
   unsigned blocks = 0;
   AqlDevice *adv = nullptr;
-  // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default
-  // kSvcBurstMax; 0: never) go to the thread's drop-in service instead of a
-  // dispatch: the kernel arguments and the descriptors travel in its mailbox
-  // (VRAM, written through the BAR), one 16-lane group per datagram, and the
-  // service stores the result word once every output is visible.
+  // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default 32, at
+  // most kSvcBurstMax; 0: never) go to the thread's drop-in service instead of
+  // a dispatch: the kernel arguments and the descriptors travel in its
+  // mailbox (VRAM, written through the BAR), one 16-lane group per datagram
+  // (32 at a time), and the service stores the result word once every output
+  // is visible.  1500 B datagrams in host memory, median per burst
+  // (profiles/r04/burst_service_r04.jsonl, burst_dispatch_r04.jsonl): 1 / 8 /
+  // 32 datagrams 8.4 / 8.8 / 10.3 us against 11.6 / 12.0 / 14.8 us for a
+  // dispatch; from 64 on the dispatch's full grid is faster.
   static const uint32_t burst_max = [] {
     const char *e = getenv("MI_CKSUM_BURST_SERVICE_MAX");
-    const long v = e ? atol(e) : (long)kSvcBurstMax;
+    const long v = e ? atol(e) : 32L;
     return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
   }();
   if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0) {

@@ -88,10 +88,10 @@ def test_service_idle_exit_and_relaunch(lib):
 
 
 def test_service_stopped_for_host_burst(lib):
-    """A host burst on the same thread goes through the same HSA queue: the
-    service is stopped first (else the burst would wait behind it), and the
-    next drop-in starts a new one."""
-    n, L, stride, first = 64, 1500, 2176, 142
+    """A host burst too large for the service (> 32 datagrams) is a dispatch
+    on the same HSA queue: the service is stopped first (else the burst would
+    wait behind it), and the next drop-in starts a new one."""
+    n, L, stride, first = 200, 1500, 2176, 142
     b = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=3)
     raw = np.zeros(b["buf"].size + 4096, np.uint8)
     s = (-raw.ctypes.data) % 4096
@@ -205,12 +205,12 @@ def test_breakdown_stamps(lib, service):
 
 
 def test_small_host_bursts_through_the_service(lib, demux_golden):
-    """Host-memory bursts of at most 128 datagrams go to the thread's service
+    """Host-memory bursts of at most 32 datagrams go to the thread's service
     (arguments and descriptors in its mailbox), larger ones to a dispatch:
     the reference-generated demux golden (TCP / UDP / ICMP / IGMP / CARP,
     options, fragments, bad sums, malformed headers) in bursts of 1-128 must
     give the golden ip / l4 / status and the same RX offload flags as one
-    720-datagram dispatch, with u64 and u32 offsets."""
+    720-datagram launch, with u64 and u32 offsets."""
     from conftest import aligned
     g = demux_golden
     keep, buf = aligned(g["ver_in"].copy(), 4096)
@@ -218,8 +218,7 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
     n = len(offs)
     mi.host_register(buf)
     try:
-        fl_all, cd_all, _ = mi.rx_offload_host(buf, n, offs=offs, lens=flen, demux=True)
-        assert lib.mi__dropin_service_live() == 0  # 720 > 128: a dispatch
+        fl_all, cd_all, _ = mi.rx_offload_host(buf, n, offs=offs, lens=flen, demux=True)  # 720 > 128: a launch
         for size in (1, 7, 32, 100, 128):
             for offs32 in (False, True):
                 ip = np.zeros(n, np.uint16); l4 = np.zeros(n, np.uint16); st = np.zeros(n, np.uint8)
@@ -228,7 +227,8 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
                     i1 = min(n, i0 + size)
                     ip[i0:i1], l4[i0:i1], st[i0:i1], _ = mi.ipv4_verify_host(
                         buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1], demux=True, offs32=offs32)
-                    assert lib.mi__dropin_service_live() == 1
+                    if i1 - i0 <= 32:
+                        assert lib.mi__dropin_service_live() == 1
                     fl[i0:i1], cd[i0:i1], _ = mi.rx_offload_host(buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1],
                                                                 demux=True, offs32=offs32)
                 assert np.array_equal(st, g["st"]), (size, offs32)
