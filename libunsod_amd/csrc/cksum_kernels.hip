@@ -117,6 +117,9 @@ template <int U>
 constexpr int multi_waves_per_simd() {
   return U == 2 ? 6 : U <= 6 ? 5 : 1;
 }
+#ifndef MI_MULTI_DESC_PF
+#define MI_MULTI_DESC_PF 0  // 1: A/B builds (VERDICT r3 asked for one measurement)
+#endif
 template <int G, int U>
 __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_verify_multi(MultiArgs a) {
   constexpr uint32_t gpw = 64u / G;
@@ -131,6 +134,12 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
   Desc d = a.e[0].d;
   uint16_t *ipo = a.e[0].ip, *l4o = a.e[0].l4;
   uint8_t *sto = a.e[0].st;
+  // MI_MULTI_DESC_PF: the descriptor (offset, length) of the wave's next unit
+  // in the same batch is loaded under this unit's data loads, so the next
+  // unit's first pass issues without a dependent descriptor round trip.
+  // (fixed-length batches only: a prefetched length would cost the U == 2
+  // shapes a spilled VGPR at their 6-wave bound)
+  uint32_t poff = ~0u;  // ~0u: nothing prefetched (pkt_off never returns it)
   for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
     if (u >= next) {
       do {
@@ -142,13 +151,21 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
       ipo = a.e[j].ip;
       l4o = a.e[j].l4;
       sto = a.e[j].st;
+      poff = ~0u;
     }
     const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
     const uint32_t i = (u - u0) * gpw + gid;
     if (i >= d.n) continue;  // the batch's last unit: whole groups drop out
-    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    const uint32_t off = poff != ~0u ? poff : pkt_off(d, i), flen = pkt_len(d, i);
     u32x4 v[U];
     issue_first<G, U>(r, off, flen, lane, v);
+#if MI_MULTI_DESC_PF
+    {
+      const uint32_t un = u + nwaves, in = (un - u0) * gpw + gid;
+      poff = ~0u;
+      if (!d.lens && un < next && un < a.units && in < d.n) poff = pkt_off(d, in);
+    }
+#endif
     IpHdr ih;
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;

@@ -736,6 +736,36 @@ def test_verify_multi_matches_single(shape):
         mi.set_shape(0, 0, 0)
 
 
+@pytest.mark.parametrize("offs32", [False, True])
+def test_verify_multi_offset_arrays(offs32):
+    """The multi-batch launch over batches described by offset arrays with a
+    fixed length (the descriptor of a wave's next unit is prefetched inside a
+    batch, never across one): offsets in shuffled slot order, batch sizes that
+    end mid-unit, one launch; every output == the oracle's for its slot."""
+    rng = np.random.default_rng(808)
+    batches, outs, want = [], [], []
+    for n, L, stride, first in [(5000, 1500, 2176, 142), (33, 1500, 2176, 142), (4099, 600, 640, 2),
+                                (1, 1500, 2176, 142), (2500, 9000, 9216, 142)]:
+        b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=n + 3 * L, payload="pattern")
+        h = b0["buf"]
+        ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
+        for i in rng.choice(n, max(1, n // 40), replace=False):
+            h[first + int(i) * stride + int(rng.integers(0, L))] ^= 0x41
+        offs = first + rng.permutation(n).astype(np.int64) * stride
+        want.append(ORC.ipv4_verify_batch(h, n, offs=offs, fixed_flen=L))
+        batches.append(mi.PktBatch(dev_tensor(h), n, offs=dev_tensor(offs), fixed_len=L, offs32=offs32))
+        outs.append(dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                         l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                         status=torch.zeros(n, dtype=torch.uint8, device="cuda")))
+    bad = torch.zeros(1, dtype=torch.int32, device="cuda")
+    mi.ipv4_verify_multi(batches, outs, bad=bad)
+    torch.cuda.synchronize()
+    for w, o in zip(want, outs):
+        assert np.array_equal(cpu(o["ip"]), w[0]) and np.array_equal(cpu(o["l4"]), w[1])
+        assert np.array_equal(cpu(o["status"]), w[2])
+    assert int(bad.item()) == sum(int((w[2] != 0).sum()) for w in want)
+
+
 def test_repeat_handle_outputs_and_rotation():
     """mi_cksum_repeat_*: every pass writes exactly what mi_cksum_ipv4_verify
     writes for its batch; runs continue the batch rotation; timed runs give a
