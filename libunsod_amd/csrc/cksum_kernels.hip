@@ -1510,10 +1510,13 @@ struct BurstArgs {
   uint32_t *bad;
 };
 constexpr uint32_t kSvcBurstMax = 128;  // datagrams (descriptors inline: 128 + 12 x 128 bytes)
+#ifndef MI_SVC_BURST_G
+#define MI_SVC_BURST_G 16  // lanes per datagram in a service burst (8: 64 datagrams per round)
+#endif
 // The burst, one 16-lane group per datagram (verify_body's per-datagram work:
 // ip_input.c:459-471 + tcp_input.c:697-720 / the RX offload flags).
 __device__ __forceinline__ void svc_burst(const BurstArgs &a) {
-  constexpr int G = 16, U = 6;
+  constexpr int G = MI_SVC_BURST_G, U = 1536 / (16 * MI_SVC_BURST_G);  // 1536 bytes per pass
   const Desc &d = a.d;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
