@@ -1511,9 +1511,9 @@ struct BurstArgs {
 };
 constexpr uint32_t kSvcBurstMax = 128;  // datagrams (descriptors inline: 128 + 12 x 128 bytes)
 #ifndef MI_SVC_BURST_G
-#define MI_SVC_BURST_G 16  // lanes per datagram in a service burst (8: 64 datagrams per round)
+#define MI_SVC_BURST_G 8  // lanes per datagram in a service burst: 64 datagrams per round (16: 32)
 #endif
-// The burst, one 16-lane group per datagram (verify_body's per-datagram work:
+// The burst, one lane group per datagram (verify_body's per-datagram work:
 // ip_input.c:459-471 + tcp_input.c:697-720 / the RX offload flags).
 __device__ __forceinline__ void svc_burst(const BurstArgs &a) {
   constexpr int G = MI_SVC_BURST_G, U = 1536 / (16 * MI_SVC_BURST_G);  // 1536 bytes per pass
@@ -4093,18 +4093,19 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   int id = -1;
   unsigned blocks = 0;
   AqlDevice *adv = nullptr;
-  // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default 32, at
+  // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default 64, at
   // most kSvcBurstMax; 0: never) go to the thread's drop-in service instead of
   // a dispatch: the kernel arguments and the descriptors travel in its
-  // mailbox (VRAM, written through the BAR), one 16-lane group per datagram
-  // (32 at a time), and the service stores the result word once every output
+  // mailbox (VRAM, written through the BAR), one 8-lane group per datagram
+  // (64 at a time), and the service stores the result word once every output
   // is visible.  1500 B datagrams in host memory, median per burst
-  // (profiles/r04/burst_service_r04.jsonl, burst_dispatch_r04.jsonl): 1 / 8 /
-  // 32 datagrams 8.4 / 8.8 / 10.3 us against 11.6 / 12.0 / 14.8 us for a
-  // dispatch; from 64 on the dispatch's full grid is faster.
+  // (profiles/r04/burst_service_lanes_r04.jsonl, burst_dispatch_r04.jsonl):
+  // 1 / 32 / 64 datagrams 8.4-8.7 / 9.3-9.7 / 12.0-12.4 us against 11.6 /
+  // 14.8 / 15.1 us for a dispatch; at 128 the dispatch's full grid is faster
+  // (16.5 against 18.1-18.9).
   static const uint32_t burst_max = [] {
     const char *e = getenv("MI_CKSUM_BURST_SERVICE_MAX");
-    const long v = e ? atol(e) : 32L;
+    const long v = e ? atol(e) : 64L;
     return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
   }();
   if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0) {

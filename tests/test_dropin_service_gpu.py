@@ -88,7 +88,7 @@ def test_service_idle_exit_and_relaunch(lib):
 
 
 def test_service_stopped_for_host_burst(lib):
-    """A host burst too large for the service (> 32 datagrams) is a dispatch
+    """A host burst too large for the service (> 64 datagrams) is a dispatch
     on the same HSA queue: the service is stopped first (else the burst would
     wait behind it), and the next drop-in starts a new one."""
     n, L, stride, first = 200, 1500, 2176, 142
@@ -205,7 +205,7 @@ def test_breakdown_stamps(lib, service):
 
 
 def test_small_host_bursts_through_the_service(lib, demux_golden):
-    """Host-memory bursts of at most 32 datagrams go to the thread's service
+    """Host-memory bursts of at most 64 datagrams go to the thread's service
     (arguments and descriptors in its mailbox), larger ones to a dispatch:
     the reference-generated demux golden (TCP / UDP / ICMP / IGMP / CARP,
     options, fragments, bad sums, malformed headers) in bursts of 1-128 must
@@ -227,7 +227,7 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
                     i1 = min(n, i0 + size)
                     ip[i0:i1], l4[i0:i1], st[i0:i1], _ = mi.ipv4_verify_host(
                         buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1], demux=True, offs32=offs32)
-                    if i1 - i0 <= 32:
+                    if i1 - i0 <= 64:
                         assert lib.mi__dropin_service_live() == 1
                     fl[i0:i1], cd[i0:i1], _ = mi.rx_offload_host(buf, i1 - i0, offs=offs[i0:i1], lens=flen[i0:i1],
                                                                 demux=True, offs32=offs32)
