@@ -2314,8 +2314,16 @@ bool debug_queues() {
   }();
   return on;
 }
+// the address ranges the library hands to its kernels (with the queues: a
+// fault address can then be told apart from the library's own buffers)
+void dbg_mem(const char *what, const void *p, size_t n) {
+  if (debug_queues()) fprintf(stderr, "libmicksum: mem %s %p +%zu\n", what, p, n);
+}
+// (an error is always reported: it is rare, and it tells a device-wide fault
+// that HIP reports later, at some unrelated call, from one of the library's
+// own queues)
 void aql_queue_error(hsa_status_t st, hsa_queue_t *q, void *slot) {
-  if (debug_queues()) fprintf(stderr, "libmicksum: HSA queue %p error 0x%x\n", (void *)q, (unsigned)st);
+  fprintf(stderr, "libmicksum: HSA queue %p error 0x%x\n", (void *)q, (unsigned)st);
   if (slot) static_cast<std::atomic<int> *>(slot)->store((int)st);
 }
 int aql_queue_create(hsa_agent_t agent, uint32_t size, std::atomic<int> *err, hsa_queue_t **q) {
@@ -2540,7 +2548,10 @@ void aql_free(AqlRun *a) {
   for (auto *&q : a->q) aql_queue_destroy(q);
   if (a->have_first) (void)hsa_signal_destroy(a->first);
   if (a->have_rest) (void)hsa_signal_destroy(a->rest);
-  if (a->kargs) (void)hipFree(a->kargs);
+  if (a->kargs) {
+    dbg_mem("aql-kargs-free", a->kargs, 0);
+    (void)hipFree(a->kargs);
+  }
   delete a;
 }
 
@@ -2615,6 +2626,7 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
   std::vector<uint8_t> host((size_t)slot * nb, 0);
   a->pkt.resize(nb);
   hipError_t e = hipMalloc((void **)&a->kargs, host.size());
+  dbg_mem("aql-kargs", a->kargs, host.size());
   if (e != hipSuccess) {
     aql_free(a);
     return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
@@ -2923,6 +2935,7 @@ bool aql_one_release(AqlOne &o) {
     if (aql_one_quiesce(o) == 0) {
       aql_queue_destroy(o.q);
       if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
+      dbg_mem("one-karg-free", o.karg, 0);
       if (o.karg) (void)hipHostFree(o.karg);
       if (o.mbox && o.mbox_dev) mbox_free(o.dev, o.mbox);
       delete o.err;
@@ -3041,6 +3054,7 @@ uint32_t *mbox_alloc(AqlDevice *a) {
         hsa_amd_memory_pool_allocate(a->mbox_pool, 4096u * kMboxSlots, 0, &p) == HSA_STATUS_SUCCESS && p) {
       if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
         a->mbox_slab = (uint8_t *)p;
+        dbg_mem("mbox-slab", p, 4096u * kMboxSlots);
       } else {
         (void)hsa_amd_memory_pool_free(p);
       }
@@ -3079,6 +3093,7 @@ int aql_one_open(AqlOne &o) {
       aql_one_release(o);
       return set_err(-ENOMEM, "AQL engine: kernel-argument slots");
     }
+    dbg_mem("one-karg", o.karg, 512 * kAqlOneSlots);
     o.device = t_ctx.device;
     thread_exit_register();
   }
@@ -3884,6 +3899,7 @@ int mi_cksum_host_register(void *p, uint64_t bytes) {
   int rc = ensure_ctx();
   if (rc) return rc;
   HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  dbg_mem("host-register", p, bytes);
   // the mapping covers whole pages
   const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + bytes + 4095) & ~(uintptr_t)4095;
   std::lock_guard<std::mutex> g(g_reg_mu);
@@ -3901,6 +3917,7 @@ int mi_cksum_host_unregister(void *p) {
         break;
       }
   }
+  dbg_mem("host-unregister", p, 0);
   HIP_TRY(hipHostUnregister(p));
   return 0;
 }
@@ -3948,6 +3965,7 @@ static int ensure_sout(ThreadCtx &c) {
   HIP_TRY(hipHostMalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
   memset(c.sout, 0, 4096);
+  dbg_mem("sout", c.sout_dev, 4096);
   return 0;
 }
 static int svc_open(ThreadCtx &c, AqlOne &o) {
@@ -4037,6 +4055,7 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     while (cap < need) cap <<= 1;
     HIP_TRY(hipHostMalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer((void **)&c.zhost_dev, c.zhost, 0));
+    dbg_mem("zhost", c.zhost_dev, cap);
     c.zhost_cap = cap;
   }
   if (!c.hstream[0])
@@ -4459,7 +4478,10 @@ uint8_t *mi__scalar_staging(size_t need) {
       set_err(-EIO, "scalar staging: stream");
       return nullptr;
     }
-    if (c.stage) (void)hipHostFree(c.stage);
+    if (c.stage) {
+      dbg_mem("stage-free", c.stage_dev, 0);
+      (void)hipHostFree(c.stage);
+    }
     c.stage = c.stage_dev = nullptr;
     c.stage_cap = 0;
     size_t cap = 1;
@@ -4471,6 +4493,7 @@ uint8_t *mi__scalar_staging(size_t need) {
       return nullptr;
     }
     c.stage_cap = cap;
+    dbg_mem("stage", c.stage_dev, cap);
   }
   return c.stage;
 }
