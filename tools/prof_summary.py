@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 kernel trace (CSV) for the checksum kernels.
 
-    python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv [--kernel k_ipv4_verify]
+    python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv [--kernel NAME]
         [--pmc-fetch DIR/run_counter_collection.csv] [--pmc-write ...]
 
-Per kernel: dispatches, mean / median duration.  For the verify kernel also the
+Per kernel: dispatches, mean / median duration.  For the verify kernel (by
+default the k_ipv4_verify* kernel with the most dispatches: k_ipv4_verify for
+1500 / 9000 B, k_ipv4_verify_slot64 for 64 B slots, k_ipv4_verify_packed or
+k_ipv4_verify_run_dma for Pareto) also the
 GPU time per launch = union of its dispatch intervals / dispatches -- when
 launches on several streams overlap, per-dispatch durations double-count the
 shared time and the union is what bench.py's hipEvent span measures.  With PMC
@@ -53,7 +56,7 @@ def pmc(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="k_ipv4_verify")
+    ap.add_argument("--kernel", default=None, help="kernel whose bursts to report (default: see above)")
     ap.add_argument("--pmc-fetch")
     ap.add_argument("--pmc-write")
     ap.add_argument("--skip-first", type=int, default=0, help="ignore the first N dispatches of the kernel")
@@ -68,6 +71,9 @@ def main():
         d = [e - s for s, e in iv]
         res[k] = dict(dispatches=len(iv), mean_us=round(statistics.mean(d) / 1e3, 3),
                       median_us=round(statistics.median(d) / 1e3, 3))
+    if a.kernel is None:
+        cand = [k for k in per if k.startswith("k_ipv4_verify")]
+        a.kernel = max(cand, key=lambda k: len(per[k])) if cand else ""
     iv = sorted(per.get(a.kernel, []))[a.skip_first:]
     if iv:
         # split into bursts separated by > 1 ms idle (warmup / timed / isolated phases)
