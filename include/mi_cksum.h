@@ -141,6 +141,10 @@ int mi_cksum_set_run_kernel(int chunks, int slots);
  * fault.
  */
 #define MI_BATCH_MAX_BYTES 0xFFFFE000ull
+/* At most this many packets (spans, chains, frames) per batch: every
+ * per-packet array -- offsets (8 B each), lengths, outputs -- is read and
+ * written through a buffer resource with 32-bit byte offsets (-E2BIG). */
+#define MI_BATCH_MAX_N 0x1FFFFE00u
 typedef struct mi_pkt_batch {
 	void           *base;
 	uint64_t        bytes;
@@ -229,7 +233,8 @@ typedef struct mi_chain_batch {
 	const uint32_t *dst;
 	const uint8_t  *proto;
 	uint32_t        max_seg;
-	uint32_t        reserved;
+	uint32_t        nseg;   /* entries of seg_off / seg_len; 0 = unknown: the
+	                           allocation holding each table bounds it */
 } mi_chain_batch;
 
 int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream);

@@ -92,7 +92,7 @@ class ChainBatchC(C.Structure):
         ("dst", C.c_void_p),
         ("proto", C.c_void_p),
         ("max_seg", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("nseg", C.c_uint32),
     ]
 
 

@@ -282,7 +282,7 @@ def chain_batch(cb: ChainBatch, length, skip, *, src=None, dst=None, proto=None,
                     cb.pkt_seg.data_ptr(), cb.n, MI_CHAIN_PSEUDO if pseudo else MI_CHAIN_SKIP,
                     keep[0].data_ptr(), keep[1].data_ptr(),
                     *([keep[2].data_ptr(), keep[3].data_ptr(), keep[4].data_ptr()] if pseudo else [None] * 3),
-                    cb.max_seg, 0)
+                    cb.max_seg, cb.seg_len.numel())
     check("mi_cksum_chain_batch", load().mi_cksum_chain_batch(C.byref(c), out.data_ptr(), C.c_void_p(_stream(stream))))
     return out
 

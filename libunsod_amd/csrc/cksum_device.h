@@ -149,18 +149,131 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const Desc &d) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(d.base), 0, (int)d.bytes,
                                            0x00020000);
 }
-// MI_BATCH_OFFS32: offs holds u32 offsets (half the descriptor bytes); the
-// flag is a kernel argument, so the branch is uniform.
+
+// ------------------------------------------------------------ bounded arrays
+//
+// Every array a kernel of this library reads or writes -- the packets (rsrc_of
+// above), the descriptors (offsets, lengths, chain and TX tables, seeds), the
+// outputs, the bad counter, the drop-in mailbox and result words, the
+// multi-batch argument table -- is reached through a buffer resource that
+// carries the array's extent.  The hardware range-checks every access against
+// it: past the extent a load reads zeros and a store or atomic is dropped.  So
+// no index -- one read from a descriptor, a stale one, a wrong one -- can
+// address memory outside the arrays the caller handed over, and no kernel has
+// a global_ / flat_ / scratch_ memory instruction or a scalar load through a
+// user pointer (tools/isa_audit.py; tests/test_isa_audit.py reads the built
+// code object on every build).  Extents: n elements for the per-datagram
+// arrays (the host keeps n * 8 below 4 GiB, make_desc), what the host measured
+// for the others (the chain / TX segment tables: the allocation holding them,
+// alloc_extent).  A NULL array has extent 0.
+//
+// MI_DEBUG_BOUNDS=1 (`make debug`, lib/debug/libmicksum.so): every access
+// through an Arr that falls outside its extent -- other than the kOOB
+// sentinel the kernels use for "no access" -- is reported with a device printf
+// naming the function and line, the offset, the extent and the lane.
+#ifndef MI_DEBUG_BOUNDS
+#define MI_DEBUG_BOUNDS 0
+#endif
+struct Arr {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t bytes;
+};
+__device__ __forceinline__ Arr arr_of(const void *p, uint64_t bytes) {
+  const uint32_t b = !p ? 0u : bytes < kOOB ? (uint32_t)bytes : kOOB;
+  return {__builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)b, 0x00020000), b};
+}
+#if MI_DEBUG_BOUNDS
+#define MI_AT , const char *fn_ = __builtin_FUNCTION(), int line_ = __builtin_LINE()
+#define MI_AT_FWD , fn_, line_
+__device__ __noinline__ void arr_oob(const char *fn, int line, uint32_t off, uint32_t size, uint32_t bytes) {
+  printf("libmicksum: out-of-range access in %s:%d: offset %u + %u of an array of %u bytes (block %u thread %u)\n",
+         fn, line, off, size, bytes, blockIdx.x, threadIdx.x);
+}
+#define ARR_CHECK(a, off, size) \
+  do { if ((off) < kOOB && (uint64_t)(off) + (size) > (a).bytes) arr_oob(fn_, line_, (off), (size), (a).bytes); } while (0)
+#else
+#define MI_AT
+#define MI_AT_FWD
+#define ARR_CHECK(a, off, size) do { } while (0)
+#endif
+// Cache policies (gfx950 CPol bits): 0 default; kSys = sc0 | sc1, the
+// system-scope coherent access a relaxed __hip_atomic at system scope compiles
+// to (the host-shared mailbox and result words); bit 31 volatile (a poll the
+// compiler must not hoist).
+constexpr int kSys = 1 | 16, kVolatile = (int)(1u << 31);
+template <int AUX = 0>
+__device__ __forceinline__ uint32_t ld_u32(const Arr &a, uint32_t i MI_AT) {
+  ARR_CHECK(a, 4u * i, 4u);
+  return __builtin_amdgcn_raw_buffer_load_b32(a.r, 4u * i, 0, AUX);
+}
+__device__ __forceinline__ uint64_t ld_u64(const Arr &a, uint32_t i MI_AT) {
+  ARR_CHECK(a, 8u * i, 8u);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(a.r, 8u * i, 0, 0);
+  return (uint64_t)v.x | ((uint64_t)v.y << 32);
+}
+__device__ __forceinline__ uint32_t ld_u8(const Arr &a, uint32_t i MI_AT) {
+  ARR_CHECK(a, i, 1u);
+  return __builtin_amdgcn_raw_buffer_load_b8(a.r, i, 0, 0);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st_u32(const Arr &a, uint32_t i, uint32_t v MI_AT) {
+  ARR_CHECK(a, 4u * i, 4u);
+  __builtin_amdgcn_raw_buffer_store_b32(v, a.r, 4u * i, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st_u64(const Arr &a, uint32_t i, uint64_t v MI_AT) {
+  ARR_CHECK(a, 8u * i, 8u);
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, a.r, 8u * i, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st_u16(const Arr &a, uint32_t i, uint32_t v MI_AT) {
+  ARR_CHECK(a, 2u * i, 2u);
+  __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, a.r, 2u * i, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void st_u8(const Arr &a, uint32_t i, uint32_t v MI_AT) {
+  ARR_CHECK(a, i, 1u);
+  __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, a.r, i, 0, AUX);
+}
+__device__ __forceinline__ void add_u32(const Arr &a, uint32_t i, uint32_t v MI_AT) {
+  ARR_CHECK(a, 4u * i, 4u);
+  (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)v, a.r, (int)(4u * i), 0, 0);
+}
+
+// A wave-uniform struct of dwords at byte `off` of an array (the multi-batch
+// argument table, a burst's arguments): vector loads, each dword made uniform
+// (so the fields can build buffer resources without a waterfall loop).
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const Arr &a, uint32_t off) {
+  static_assert(sizeof(T) % 4 == 0, "dwords");
+  uint32_t w[sizeof(T) / 4];
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(T) / 4; ++k)
+    w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(a.r, off + 4u * k, 0, 0));
+  T t;
+  __builtin_memcpy(&t, w, sizeof t);
+  return t;
+}
+
+// The batch's descriptor arrays: n offsets (u64, or u32 with MI_BATCH_OFFS32)
+// and n lengths.  The flag is a kernel argument, so the branch is uniform.
+__device__ __forceinline__ Arr offs_arr(const Desc &d) {
+  return arr_of(d.offs, (uint64_t)d.n * ((d.flags & MI_BATCH_OFFS32) ? 4u : 8u));
+}
+__device__ __forceinline__ Arr lens_arr(const Desc &d) { return arr_of(d.lens, (uint64_t)d.n * 4u); }
 __device__ __forceinline__ uint64_t desc_off(const Desc &d, uint32_t i) {
   if (!d.offs) return d.first_off + (uint64_t)i * d.stride;
-  return (d.flags & MI_BATCH_OFFS32) ? (uint64_t)reinterpret_cast<const uint32_t *>(d.offs)[i] : d.offs[i];
+  const Arr a = offs_arr(d);
+  return (d.flags & MI_BATCH_OFFS32) ? (uint64_t)ld_u32(a, i) : ld_u64(a, i);
 }
 __device__ __forceinline__ uint32_t pkt_off(const Desc &d, uint32_t i) {
   const uint64_t o = desc_off(d, i);
   return o < kOOB ? (uint32_t)o : kOOB;
 }
 __device__ __forceinline__ uint32_t pkt_len(const Desc &d, uint32_t i) {
-  const uint32_t l = d.lens ? d.lens[i] : d.fixed_len;
+  const uint32_t l = d.lens ? ld_u32(lens_arr(d), i) : d.fixed_len;
   return l < 0x7fff0000u ? l : 0x7fff0000u;
 }
 // Packet bytes are read once: nontemporal loads (aux = 2, `nt`) measured +10 %
@@ -242,6 +355,19 @@ struct SpanSeeds {
   const uint8_t *proto;
   const uint32_t *plens;
 };
+// Span i's output from its folded bytes S (stream lanes): the seeds (n-element
+// arrays) added, folded, complemented, stored into out (n u16).
+__device__ __forceinline__ void span_emit(const Desc &d, const SpanSeeds &s, uint32_t i, uint32_t len, uint64_t sum,
+                                          uint16_t *out) {
+  const uint64_t n4 = (uint64_t)d.n * 4u;
+  if (s.seeds) sum += ld_u32(arr_of(s.seeds, n4), i);
+  if (s.src) {
+    const uint32_t pl = s.plens ? ld_u32(arr_of(s.plens, n4), i) : len;
+    sum += (uint64_t)ld_u32(arr_of(s.src, n4), i) + ld_u32(arr_of(s.dst, n4), i) +
+           (ld_u8(arr_of(s.proto, d.n), i) << 8) + swap16(pl & 0xffffu);
+  }
+  st_u16(arr_of(out, (uint64_t)d.n * 2u), i, ~fold16_64(sum) & 0xffffu);
+}
 
 template <int G, int U>
 __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, SpanSeeds s,
@@ -271,12 +397,7 @@ __global__ __launch_bounds__(kBlock) void k_span(Desc d, uint32_t abs_lanes, Spa
     if (lane == 0) {
       uint64_t sum = fold16(acc);
       if (!abs_lanes && (((uintptr_t)d.base + off) & 1u)) sum = swap16((uint32_t)sum);
-      if (s.seeds) sum += s.seeds[i];
-      if (s.src) {
-        const uint32_t pl = s.plens ? s.plens[i] : len;
-        sum += (uint64_t)s.src[i] + s.dst[i] + ((uint32_t)s.proto[i] << 8) + swap16(pl & 0xffffu);
-      }
-      out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+      span_emit(d, s, i, len, sum, out);
     }
   }
 }
@@ -379,7 +500,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
     const uint32_t nwaves = gridDim.x * (kBlock / 64);
     for (uint32_t base = (blockIdx.x * (kBlock / 64) + wv) * 64u; base < d.n; base += nwaves * 64u) {
       const uint32_t k = base + lane64;
-      const uint32_t l = k < d.n ? d.lens[k] : 0u;
+      const uint32_t l = k < d.n ? ld_u32(lens_arr(d), k) : 0u;
       const bool in = k < d.n && l >= d.len_lo && l < d.len_hi;
       const uint64_t m = __ballot(in);
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
@@ -570,12 +691,12 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
 #define MI_DEFER 0
 #endif
 constexpr bool kDefer = MI_DEFER;
-// MI_OUT_AUX >= 0: the ip / l4 / status stores as buffer stores with that
-// cache policy (gfx950 CPol bits: 1 = sc0, 2 = nt, 16 = sc1); -1 (default):
-// plain global stores.  Measured (profiles/r03/serial_floor_r03.jsonl), 1500 B
-// verify per launch on one stream / two queues: default 18.5 / 14.24, sc0
-// 18.3-18.7, sc1 19.3-19.6 / 15.0, sc0+sc1 19.2-19.6 / 15.1, nt 20.2-20.7 /
-// 18.5-18.7 (partial-line nt writes) -- plain stores stay.
+// MI_OUT_AUX: the cache policy of the ip / l4 / status buffer stores (gfx950
+// CPol bits: 1 = sc0, 2 = nt, 16 = sc1; -1 or 0: default).  Measured
+// (profiles/r03/serial_floor_r03.jsonl), 1500 B verify per launch on one stream
+// / two queues: default 18.5 / 14.24, sc0 18.3-18.7, sc1 19.3-19.6 / 15.0,
+// sc0+sc1 19.2-19.6 / 15.1, nt 20.2-20.7 / 18.5-18.7 (partial-line nt writes),
+// plain global stores 18.3-18.9 -- the default policy stays.
 #ifndef MI_OUT_AUX
 #define MI_OUT_AUX -1
 #endif
@@ -615,29 +736,22 @@ __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr 
   return o;
 }
 
+// The stores: each output through a resource over its n elements (bad: one
+// counter), so a datagram index can only ever land inside its own array.
+// (Plain global stores and buffer stores of the default policy measured the
+// same, profiles/r03/serial_floor_r03.jsonl.)
 __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const Desc &d) {
   if (o.i == ~0u) return;
-#if MI_OUT_AUX >= 0
-  constexpr int kOA = MI_OUT_AUX;
-  if (ip_out)
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o.ip, __builtin_amdgcn_make_buffer_rsrc(ip_out, 0, 0x7fffffff, 0x00020000),
-                                          2u * o.i, 0, kOA);
-  if (l4_out)
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)o.l4, __builtin_amdgcn_make_buffer_rsrc(l4_out, 0, 0x7fffffff, 0x00020000),
-                                          2u * o.i, 0, kOA);
-  if (st_out)
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)o.st, __builtin_amdgcn_make_buffer_rsrc(st_out, 0, 0x7fffffff, 0x00020000),
-                                         o.i, 0, kOA);
-#else
-  if (ip_out) ip_out[o.i] = (uint16_t)o.ip;
-  if (l4_out) l4_out[o.i] = (uint16_t)o.l4;
-  if (st_out) st_out[o.i] = (uint8_t)o.st;
-#endif
-  if (bad && (o.st & ~MI_ST_L4_NONE)) atomicAdd(bad, 1u);
+  constexpr int kOA = MI_OUT_AUX >= 0 ? MI_OUT_AUX : 0;
+  const uint64_t n = d.n;
+  if (ip_out) st_u16<kOA>(arr_of(ip_out, 2u * n), o.i, o.ip);
+  if (l4_out) st_u16<kOA>(arr_of(l4_out, 2u * n), o.i, o.l4);
+  if (st_out) st_u8<kOA>(arr_of(st_out, n), o.i, o.st);
+  if (bad && (o.st & ~MI_ST_L4_NONE)) add_u32(arr_of(bad, 4u), 0u, 1u);
   if (d.cflags) {
-    d.cflags[o.i] = o.fl;
-    if (d.cdata) d.cdata[o.i] = o.cd;
+    st_u32(arr_of(d.cflags, 4u * n), o.i, o.fl);
+    if (d.cdata) st_u32(arr_of(d.cdata, 4u * n), o.i, o.cd);
   }
 }
 

@@ -126,31 +126,45 @@ __global__ __launch_bounds__(kBlock, multi_waves_per_simd<U>()) void k_ipv4_veri
   const int lane = threadIdx.x & (G - 1);
   const uint32_t gid = (threadIdx.x & 63u) / G;
   const uint32_t nwaves = gridDim.x * (kBlock / 64);
+  // The argument table is read through a resource over the kernel-argument
+  // segment (a runtime batch index into a by-value table would otherwise be an
+  // unchecked load, or a copy of the whole table into scratch).
+  const Arr tab = arr_of((const void *)__builtin_amdgcn_kernarg_segment_ptr(), sizeof(MultiArgs));
+  auto ent = [&](uint32_t k) {
+    return ld_uniform<MultiEnt>(tab, (uint32_t)(offsetof(MultiArgs, e) + sizeof(MultiEnt) * k));
+  };
+  auto unit0 = [&](uint32_t k) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)ld_u32(tab, (uint32_t)(offsetof(MultiArgs, e) + sizeof(MultiEnt) * k + offsetof(MultiEnt, unit0)) / 4u));
+  };
   // A wave's units only move forward, so its batch does too: the batch's
   // descriptor is copied out of the argument table once per batch change, not
   // re-read (a scalar-load round trip ahead of the data loads) per unit.
-  uint32_t j = 0, u0 = a.e[0].unit0;
-  uint32_t next = a.nb > 1 ? a.e[1].unit0 : 0xffffffffu;
-  Desc d = a.e[0].d;
-  uint16_t *ipo = a.e[0].ip, *l4o = a.e[0].l4;
-  uint8_t *sto = a.e[0].st;
+  MultiEnt e0 = ent(0);
+  uint32_t j = 0, u0 = e0.unit0;
+  uint32_t next = a.nb > 1 ? unit0(1) : 0xffffffffu;
+  Desc d = e0.d;
+  uint16_t *ipo = e0.ip, *l4o = e0.l4;
+  uint8_t *sto = e0.st;
   // MI_MULTI_DESC_PF: the descriptor (offset, length) of the wave's next unit
   // in the same batch is loaded under this unit's data loads, so the next
   // unit's first pass issues without a dependent descriptor round trip.
   // (fixed-length batches only: a prefetched length would cost the U == 2
   // shapes a spilled VGPR at their 6-wave bound)
   uint32_t poff = ~0u;  // ~0u: nothing prefetched (pkt_off never returns it)
-  for (uint32_t u = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6); u < a.units; u += nwaves) {
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (uint32_t u = blockIdx.x * (kBlock / 64) + wv; u < a.units; u += nwaves) {
     if (u >= next) {
       do {
         ++j;
-      } while (j + 1 < a.nb && a.e[j + 1].unit0 <= u);
-      d = a.e[j].d;
-      u0 = a.e[j].unit0;
-      next = j + 1 < a.nb ? a.e[j + 1].unit0 : 0xffffffffu;
-      ipo = a.e[j].ip;
-      l4o = a.e[j].l4;
-      sto = a.e[j].st;
+      } while (j + 1 < a.nb && unit0(j + 1) <= u);
+      const MultiEnt e = ent(j);
+      d = e.d;
+      u0 = e.unit0;
+      next = j + 1 < a.nb ? unit0(j + 1) : 0xffffffffu;
+      ipo = e.ip;
+      l4o = e.l4;
+      sto = e.st;
       poff = ~0u;
     }
     const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
@@ -280,17 +294,11 @@ __device__ __forceinline__ void chunk_put_byte(u32x4 &v, int b, uint32_t x) {
 // One span's output (k_span's epilogue): the absolute-lane sum S of its bytes,
 // swapped to stream lanes when the span starts odd (in_cksum.c:222-225), plus
 // the seeds, folded and complemented.
-__device__ __forceinline__ void span_store(uint32_t i, uint32_t off, uint32_t len, bool swap, uint32_t S,
+__device__ __forceinline__ void span_store(const Desc &d, uint32_t i, uint32_t len, bool swap, uint32_t S,
                                            const SpanSeeds &s, uint16_t *out) {
-  (void)off;
   uint64_t sum = fold16(S);
   if (swap) sum = swap16((uint32_t)sum);
-  if (s.seeds) sum += s.seeds[i];
-  if (s.src) {
-    const uint32_t pl = s.plens ? s.plens[i] : len;
-    sum += (uint64_t)s.src[i] + s.dst[i] + ((uint32_t)s.proto[i] << 8) + swap16(pl & 0xffffu);
-  }
-  out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+  span_emit(d, s, i, len, sum, out);
 }
 
 
@@ -395,7 +403,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
         uint64_t acc = 0;  // one lane walks the span (64-bit: any length)
         for (uint32_t c = off & ~15u; c < off + flen; c += 16u)
           acc += range_sum(ld16(r, c), (int)(c - off), 0, (int)flen);
-        span_store(i, off, flen, (((uintptr_t)d.base + off) & 1u) && !abs_lanes, fold16_64(acc), sp, ip_out);
+        span_store(d, i, flen, (((uintptr_t)d.base + off) & 1u) && !abs_lanes, fold16_64(acc), sp, ip_out);
       } else if (act) {
         u32x4 w[4];
         issue_first<1, 4>(r, off, flen, 0, w);
@@ -471,7 +479,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
       if (ce >= nch) qe = carry;  // end on the run's last chunk boundary
       if (act && SPAN) {
         const uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(hv[0], 0, 0, (int)h));
-        span_store(i, off, flen, (h & 1u) && !abs_lanes, total, sp, ip_out);
+        span_store(d, i, flen, (h & 1u) && !abs_lanes, total, sp, ip_out);
       } else if (act) {
         const IpHdr ih = parse_ipv4<1, 3>(hv, h);
         const bool odd = h & 1u;
@@ -1026,48 +1034,45 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// (bytes <= MI_BATCH_MAX_BYTES, host-checked: the whole buffer is one resource)
 __global__ __launch_bounds__(kBlock) void k_fill(uint8_t *base, uint64_t bytes, uint64_t seed) {
+  const Arr b = arr_of(base, bytes);
   const uint64_t nchunk = bytes / 16;
   for (uint64_t c = blockIdx.x * (uint64_t)kBlock + threadIdx.x; c < nchunk;
        c += (uint64_t)gridDim.x * kBlock) {
-    const uint64_t a = splitmix64(seed ^ (2 * c)), b = splitmix64(seed ^ (2 * c + 1));
-    u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
-    *reinterpret_cast<u32x4 *>(base + 16 * c) = v;
+    const uint64_t a = splitmix64(seed ^ (2 * c)), x = splitmix64(seed ^ (2 * c + 1));
+    const u32x4 v = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)x, (uint32_t)(x >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, b.r, (uint32_t)(16u * c), 0, 0);
   }
 }
 
-__device__ __forceinline__ void put_be16(uint8_t *p, uint32_t v) {
-  p[0] = (uint8_t)(v >> 8);
-  p[1] = (uint8_t)v;
-}
-
+// The synthetic IPv4 + TCP header of datagram i (40 bytes, byte k of dword
+// k / 4 little-endian), stored through the packet buffer's resource.
 __global__ __launch_bounds__(kBlock) void k_synth_hdr(Desc d) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= d.n) return;
   const uint64_t off = desc_off(d, i);
-  const uint32_t len = d.lens ? d.lens[i] : d.fixed_len;
+  const uint32_t len = d.lens ? ld_u32(lens_arr(d), i) : d.fixed_len;
   if (len < 40u || off + 40u > d.bytes) return;
-  uint8_t *p = const_cast<uint8_t *>(d.base) + off;
-  p[0] = 0x45; p[1] = 0;
-  put_be16(p + 2, len);
-  put_be16(p + 4, i & 0xffffu);
-  put_be16(p + 6, 0x4000);
-  p[8] = 64; p[9] = 6; p[10] = 0; p[11] = 0;
-  p[12] = 10; p[13] = 0; p[14] = (uint8_t)(i >> 8); p[15] = (uint8_t)i;
-  p[16] = 10; p[17] = 1; p[18] = (uint8_t)(i >> 8); p[19] = (uint8_t)i;
-  uint8_t *t = p + 20;
-  put_be16(t + 0, 40000u + (i % 1000u));
-  put_be16(t + 2, 5201);
-  put_be16(t + 4, i >> 16); put_be16(t + 6, i);  // seq
-  put_be16(t + 8, 0); put_be16(t + 10, 1);       // ack
-  t[12] = 5 << 4; t[13] = 0x10;
-  put_be16(t + 14, 65535);
+  auto be16 = [](uint32_t v) { return ((v >> 8) & 0xffu) | ((v & 0xffu) << 8); };
   // th_sum = in_pseudo(src, dst, htons(tcp_len + IPPROTO_TCP)) (tcp_output.c:1084)
   const uint32_t src = 10u | (0u << 8) | ((i >> 8) & 0xffu) << 16 | (i & 0xffu) << 24;
   const uint32_t dst = 10u | (1u << 8) | ((i >> 8) & 0xffu) << 16 | (i & 0xffu) << 24;
   const uint32_t seed = fold16_64((uint64_t)src + dst + swap16((len - 20u + 6u) & 0xffffu));
-  t[16] = (uint8_t)seed; t[17] = (uint8_t)(seed >> 8);
-  t[18] = 0; t[19] = 0;
+  const uint32_t w[10] = {
+      0x45u | be16(len) << 16,                      // ver/hl, tos, ip_len
+      be16(i & 0xffffu) | be16(0x4000u) << 16,      // ip_id, ip_off (DF)
+      64u | 6u << 8,                                // ttl, proto TCP, ip_sum 0
+      src, dst,
+      be16(40000u + (i % 1000u)) | be16(5201u) << 16,  // ports
+      be16(i >> 16) | be16(i & 0xffffu) << 16,      // seq
+      be16(0u) | be16(1u) << 16,                    // ack
+      (5u << 4) | 0x10u << 8 | be16(65535u) << 16,  // off, flags, win
+      seed & 0xffffu};                              // th_sum, urp
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const uint32_t o = (uint32_t)off;
+#pragma unroll
+  for (int k = 0; k < 40; ++k) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w[k >> 2] >> (8 * (k & 3))), r, o + k, 0, 0);
 }
 
 // ------------------------------------------------------ scatter-gather chains
@@ -1090,7 +1095,18 @@ struct ChainDesc {
   const uint32_t *src, *dst;
   const uint8_t *proto;
   uint32_t pseudo;
+  uint32_t nseg;  // segments the seg_off / seg_len tables hold (host: their allocation)
 };
+// The chain batch's tables as bounded arrays (cksum_device.h, Arr).
+struct ChainArrs {
+  Arr pkt_seg, len, skip, src, dst, proto, seg_off, seg_len, out;
+};
+__device__ __forceinline__ ChainArrs chain_arrs(const ChainDesc &cd, uint16_t *out) {
+  const uint64_t n = cd.n;
+  return {arr_of(cd.pkt_seg, 4u * (n + 1u)), arr_of(cd.len, 4u * n), arr_of(cd.skip, 4u * n),
+          arr_of(cd.src, 4u * n),           arr_of(cd.dst, 4u * n), arr_of(cd.proto, n),
+          arr_of(cd.seg_off, 8ull * cd.nseg), arr_of(cd.seg_len, 4ull * cd.nseg), arr_of(out, 2u * n)};
+}
 
 // Folded absolute-lane sum of bytes [off, off + len); valid in the group leader.
 template <int G, int U>
@@ -1141,6 +1157,7 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
   d.base = cd.base;
   d.bytes = cd.bytes;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const ChainArrs ca = chain_arrs(cd, out);
   const int lane = threadIdx.x & (G - 1);
   const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
@@ -1159,10 +1176,10 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
     kk = ke = ln = 0;
     sk = 0;
     if (j < cd.n) {
-      kk = cd.pkt_seg[j];
-      ke = cd.pkt_seg[j + 1];
-      sk = cd.skip[j];
-      ln = (uint32_t)cd.len[j];
+      kk = ld_u32(ca.pkt_seg, j);
+      ke = ld_u32(ca.pkt_seg, j + 1);
+      sk = (int32_t)ld_u32(ca.skip, j);
+      ln = ld_u32(ca.len, j);
     }
   };
   auto level2 = [&](uint32_t kk, uint32_t ke, int32_t &m, uint64_t &o) {
@@ -1170,8 +1187,8 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
     m = 0;
     o = 0;
     if ((uint32_t)lane < ns && ns <= (uint32_t)G) {
-      m = cd.seg_len[kk + lane];
-      o = cd.seg_off[kk + lane];
+      m = (int32_t)ld_u32(ca.seg_len, kk + lane);
+      o = ld_u64(ca.seg_off, kk + lane);
     }
   };
   if (MI_CHAIN_PREFETCH) {
@@ -1196,10 +1213,10 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
       so = so_c;
       level1(in, k_n, kend_n, lo_n, ln_n);
     } else {
-      k = cd.pkt_seg[i];
-      kend = cd.pkt_seg[i + 1];
-      lo = cd.skip[i];
-      ln_i = (uint32_t)cd.len[i];
+      k = ld_u32(ca.pkt_seg, i);
+      kend = ld_u32(ca.pkt_seg, i + 1);
+      lo = (int32_t)ld_u32(ca.skip, i);
+      ln_i = ld_u32(ca.len, i);
     }
     auto prefetch2 = [&]() {
       if (!MI_CHAIN_PREFETCH || pre2) return;
@@ -1215,8 +1232,8 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
     const int64_t hi = cd.pseudo ? lo + (int64_t)(int32_t)ln_i : (int64_t)(int32_t)ln_i;
     const uint32_t nseg = kend > k ? kend - k : 0u;
     if (!MI_CHAIN_PREFETCH && (uint32_t)lane < nseg && nseg <= (uint32_t)G) {
-      ml = cd.seg_len[k + lane];
-      so = cd.seg_off[k + lane];
+      ml = (int32_t)ld_u32(ca.seg_len, k + lane);
+      so = ld_u64(ca.seg_off, k + lane);
     }
     // flat only with non-negative, < 16 MiB mbufs (no u32 wrap in the scan),
     // offsets the bounds check can take, and (pseudo) off0 inside the first
@@ -1252,8 +1269,8 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
         auto nch = [](uint32_t A, uint32_t n) { return n ? ((A & 15u) + n + 15u) >> 4 : 0u; };
         const uint32_t P1 = nch(A0, N0), P2 = P1 + nch(A1, N1), P3 = P2 + nch(A2, N2), T = P3 + nch(A3, N3);
         if (cd.pseudo && nseg)
-          sum = (uint64_t)cd.src[i] + cd.dst[i] + ((uint32_t)cd.proto[i] << 8) +
-                swap16((uint32_t)cd.len[i] & 0xffffu);  // in_cksum.c:252-253
+          sum = (uint64_t)ld_u32(ca.src, i) + ld_u32(ca.dst, i) + (ld_u8(ca.proto, i) << 8) +
+                swap16(ld_u32(ca.len, i) & 0xffffu);  // in_cksum.c:252-253
         uint32_t acc = 0;
         const uint32_t npass = (T + G * U - 1) / (G * U);
         for (uint32_t p = 0; p < npass; ++p) {
@@ -1287,7 +1304,7 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
           acc = fold16(acc);
         }
         sum += fold16(group_sum<G>(acc));
-        if (lane == 0) out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+        if (lane == 0) st_u16(ca.out, i, ~fold16_64(sum) & 0xffffu);
         prefetch2();
         continue;
       }
@@ -1305,12 +1322,12 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
       clen += mlen;
     };
     if (!cd.pseudo) {
-      int64_t skip = cd.skip[i], rem = (int64_t)cd.len[i] - skip;
+      int64_t skip = (int32_t)ld_u32(ca.skip, i), rem = (int64_t)(int32_t)ld_u32(ca.len, i) - skip;
       for (; skip && k < kend; ++k) {  // in_cksum.c:204-212
-        const int64_t ml = cd.seg_len[k];
+        const int64_t ml = (int32_t)ld_u32(ca.seg_len, k);
         if (ml > skip) {
           const int64_t mlen = min(ml - skip, rem);
-          piece(cd.seg_off[k] + (uint64_t)skip, mlen);
+          piece(ld_u64(ca.seg_off, k) + (uint64_t)skip, mlen);
           rem -= mlen;
           ++k;
           skip = 0;
@@ -1320,31 +1337,31 @@ __global__ __launch_bounds__(kBlock) void k_chain(ChainDesc cd, uint16_t *out) {
       }
       if (!skip)
         for (; k < kend && rem > 0; ++k) {  // :214-229
-          const int64_t ml = cd.seg_len[k];
+          const int64_t ml = (int32_t)ld_u32(ca.seg_len, k);
           if (ml == 0) continue;
           const int64_t mlen = min(ml, rem);
-          piece(cd.seg_off[k], mlen);
+          piece(ld_u64(ca.seg_off, k), mlen);
           rem -= mlen;
         }
     } else if (k < kend) {
-      const int64_t plen = cd.len[i], off0 = cd.skip[i];
-      sum = (uint64_t)cd.src[i] + cd.dst[i] + ((uint32_t)cd.proto[i] << 8) +
+      const int64_t plen = (int32_t)ld_u32(ca.len, i), off0 = (int32_t)ld_u32(ca.skip, i);
+      sum = (uint64_t)ld_u32(ca.src, i) + ld_u32(ca.dst, i) + (ld_u8(ca.proto, i) << 8) +
             swap16((uint32_t)plen & 0xffffu);  // :252-253
-      int64_t rem = plen, mlen = (int64_t)cd.seg_len[k] - off0;
-      uint64_t a = cd.seg_off[k] + (uint64_t)off0;
+      int64_t rem = plen, mlen = (int64_t)(int32_t)ld_u32(ca.seg_len, k) - off0;
+      uint64_t a = ld_u64(ca.seg_off, k) + (uint64_t)off0;
       for (;;) {  // :254-273
         if (rem < mlen) mlen = rem;
         piece(a, mlen);
         rem -= mlen;
         do {
           ++k;
-        } while (k < kend && rem && cd.seg_len[k] == 0);
+        } while (k < kend && rem && ld_u32(ca.seg_len, k) == 0u);
         if (k >= kend || !rem) break;
-        mlen = cd.seg_len[k];
-        a = cd.seg_off[k];
+        mlen = (int32_t)ld_u32(ca.seg_len, k);
+        a = ld_u64(ca.seg_off, k);
       }
     }
-    if (lane == 0) out[i] = (uint16_t)(~fold16_64(sum) & 0xffffu);
+    if (lane == 0) st_u16(ca.out, i, ~fold16_64(sum) & 0xffffu);
   }
 }
 
@@ -1452,16 +1469,21 @@ __device__ __forceinline__ uint32_t scalar_span(const uint8_t *base, uint32_t by
 // the host first -- every read of the staging bytes has been consumed -- so
 // the untraced store is relaxed (a release at system scope would write back
 // the whole L2 first); the traced one orders the stamps before it.
+// `out` is the caller's result block: kOutWords words (the result, the two
+// stamps, the service's exit token), written through a resource over them
+// with system-scope coherent stores (what a relaxed system-scope atomic store
+// compiles to).
+constexpr uint32_t kOutWords = 8;
 __device__ __forceinline__ void scalar_result(uint32_t *out, uint32_t tag, uint32_t res, bool trace, uint64_t t0) {
   const uint32_t w = ((tag & 0xffffu) << 16) | res;
+  const Arr o = arr_of(out, 4u * kOutWords);
   if (trace) {
     const uint64_t t1 = rt_clock();
-    __hip_atomic_store((uint64_t *)(out + 2), t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store((uint64_t *)(out + 4), t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(out, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  } else {
-    __hip_atomic_store(out, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    st_u64<kSys>(o, 1u, t0);  // out[2..3]
+    st_u64<kSys>(o, 2u, t1);  // out[4..5]
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
+  st_u32<kSys>(o, 0u, w);
 }
 
 // (the same kernel serves the HIP launch and the AQL one-shot dispatch, hence
@@ -1540,6 +1562,7 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
   __shared__ uint32_t part[kScalarThreads / 64];
   __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [11] a burst, [12] served by wave 0
   __shared__ u32x4 s_args[8];   // a burst's BurstArgs
+  const Arr mb = arr_of(box, 4u * kSvcWords);  // the mailbox, read at system scope
   uint32_t last = seq0;
   uint64_t t_last = rt_clock(), t_seen = 0;
   for (;;) {
@@ -1548,7 +1571,7 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
       uint32_t sq = last;
       if (lane == 0) {
         for (;;) {
-          sq = __hip_atomic_load(box, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          sq = ld_u32<kSys | kVolatile>(mb, 0u);
           if (sq != last || rt_clock() - t_last > idle_ticks) break;
           __builtin_amdgcn_s_sleep(1);
         }
@@ -1562,13 +1585,11 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
         uint32_t f = 0;
         u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
         auto ld4 = [&](uint32_t c) {
-          const uint32_t *q = box + kSvcInline + 4u * c;
-          return u32x4{__hip_atomic_load(q + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                       __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                       __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                       __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)};
+          const uint32_t q = kSvcInline + 4u * c;
+          return u32x4{ld_u32<kSys | kVolatile>(mb, q), ld_u32<kSys | kVolatile>(mb, q + 1u),
+                       ld_u32<kSys | kVolatile>(mb, q + 2u), ld_u32<kSys | kVolatile>(mb, q + 3u)};
         };
-        if (lane >= 2 && lane < 11) f = __hip_atomic_load(box + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane >= 2 && lane < 11) f = ld_u32<kSys | kVolatile>(mb, lane);
         if (!(sq >> 31)) {
           if (lane < nck) v0 = ld4(lane);
           if (64u + lane < nck) v1 = ld4(64u + lane);
@@ -1609,15 +1630,20 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
     __syncthreads();
     const uint32_t sq = req[0];
     if (sq == last || (sq >> 31)) {  // idle, or a stop request
-      if (threadIdx.x == 0) __hip_atomic_store(out + 6, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (threadIdx.x == 0) st_u32<kSys>(arr_of(out, 4u * kOutWords), 6u, token);
       break;
     }
     if (req[11]) {
       // a host RX burst: every wave, then the result word once every wave's
       // outputs are visible at system scope
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      // the arguments, wave-uniform (they build the burst's resources)
+      uint32_t w[sizeof(BurstArgs) / 4];
+#pragma unroll
+      for (uint32_t k = 0; k < sizeof(BurstArgs) / 4; ++k)
+        w[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)((const uint32_t *)s_args)[k]);
       BurstArgs a;
-      __builtin_memcpy(&a, (const void *)s_args, sizeof a);
+      __builtin_memcpy(&a, w, sizeof a);
       svc_burst(a);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __syncthreads();
@@ -1656,6 +1682,107 @@ int set_err(int code, const char *fmt, ...) {
                      __LINE__);                                                        \
   } while (0)
 
+// ------------------------------------------------ GPU memory-fault reporter
+//
+// A GPU page fault (an access to memory that is not mapped) reaches the
+// process asynchronously: HIP flags it and reports hipErrorIllegalAddress at
+// some later, unrelated call, without the address.  So the library keeps a
+// journal of what it handed to the GPU -- every launch or dispatch with the
+// arrays it references, every buffer it allocates or frees -- in a lock-free
+// ring, and registers an HSA system-event handler that, on a memory fault,
+// prints the faulting address and the journal entries whose ranges hold or
+// border it, newest first, plus the latest launches.  A fault is then located
+// from its one occurrence, not by rerunning until it shows again.
+struct JEnt {
+  std::atomic<uint64_t> seq{0};
+  const char *what = nullptr;  // a string literal
+  uint64_t p = 0, bytes = 0;
+  uint32_t tag = 0;
+  double t = 0;
+};
+constexpr uint32_t kJournal = 1024;
+JEnt g_journal[kJournal];
+std::atomic<uint64_t> g_jseq{0};
+double mono_s();
+void jnote(const char *what, const void *p = nullptr, uint64_t bytes = 0, uint32_t tag = 0) {
+  const uint64_t s = g_jseq.fetch_add(1, std::memory_order_relaxed) + 1;
+  JEnt &e = g_journal[s % kJournal];
+  e.seq.store(0, std::memory_order_relaxed);
+  e.what = what;
+  e.p = (uint64_t)(uintptr_t)p;
+  e.bytes = bytes;
+  e.tag = tag;
+  e.t = mono_s();
+  e.seq.store(s, std::memory_order_release);
+}
+// The library's own allocations and frees, journaled (a fault on a freed
+// buffer then names it).
+uint64_t alloc_bytes(const void *p) {
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (!p || hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return size;
+}
+template <typename T>
+hipError_t jmalloc(T **p, size_t n) {
+  const hipError_t e = hipMalloc((void **)p, n);
+  if (e == hipSuccess) jnote("alloc device", *p, n);
+  return e;
+}
+template <typename T>
+hipError_t jhostmalloc(T **p, size_t n, unsigned flags) {
+  const hipError_t e = hipHostMalloc((void **)p, n, flags);
+  if (e == hipSuccess) jnote("alloc host", *p, n);
+  return e;
+}
+hipError_t jfree(void *p) {
+  if (p) jnote("free device", p, alloc_bytes(p));
+  return hipFree(p);
+}
+hipError_t jhostfree(void *p) {
+  if (p) jnote("free host", p, alloc_bytes(p));
+  return hipHostFree(p);
+}
+hsa_status_t fault_event(const hsa_amd_event_t *ev, void *) {
+  if (!ev || ev->event_type != HSA_AMD_GPU_MEMORY_FAULT_EVENT) return HSA_STATUS_SUCCESS;
+  const uint64_t va = ev->memory_fault.virtual_address;
+  const uint32_t why = ev->memory_fault.fault_reason_mask;
+  fprintf(stderr, "libmicksum: GPU memory fault at 0x%llx (reason 0x%x%s%s%s)\n", (unsigned long long)va, why,
+          why & HSA_AMD_MEMORY_FAULT_PAGE_NOT_PRESENT ? " page-not-present" : "",
+          why & HSA_AMD_MEMORY_FAULT_READ_ONLY ? " read-only" : "", why & HSA_AMD_MEMORY_FAULT_IMPRECISE ? " imprecise" : "");
+  const uint64_t top = g_jseq.load(std::memory_order_acquire), now_t = mono_s();
+  constexpr uint64_t kNear = 1u << 20;  // ranges within 1 MiB of the address
+  int near = 0, recent = 0;
+  for (uint64_t s = top; s > 0 && s + kJournal > top; --s) {
+    const JEnt &e = g_journal[s % kJournal];
+    if (e.seq.load(std::memory_order_acquire) != s || !e.what) continue;
+    const bool hit = e.bytes && va + kNear >= e.p && va < e.p + e.bytes + kNear;
+    const bool launch = !e.p && recent < 24;
+    if (!hit && !launch) continue;
+    if (hit) ++near;
+    else ++recent;
+    fprintf(stderr, "libmicksum:   %s#%llu %.6f s ago: %s tag %u [0x%llx, +%llu)%s\n", hit ? "near " : "     ",
+            (unsigned long long)s, now_t - e.t, e.what, e.tag, (unsigned long long)e.p, (unsigned long long)e.bytes,
+            hit && va >= e.p && va < e.p + e.bytes ? "  <-- holds the address" : "");
+  }
+  fprintf(stderr, "libmicksum: %d journal ranges near the address (of the last %u events)\n", near, kJournal);
+  return HSA_STATUS_SUCCESS;
+}
+std::once_flag g_fault_once;
+std::atomic<int> g_fault_handler{0};  // 1 registered, -1 refused by the runtime
+void fault_reporter_register() {
+  std::call_once(g_fault_once, [] {
+    // (the runtime is up -- HIP started it; this takes one reference more)
+    const hsa_status_t st = hsa_init() == HSA_STATUS_SUCCESS
+                                ? hsa_amd_register_system_event_handler(fault_event, nullptr)
+                                : HSA_STATUS_ERROR_NOT_INITIALIZED;
+    g_fault_handler.store(st == HSA_STATUS_SUCCESS ? 1 : -1);
+  });
+}
+
 struct ThreadCtx {
   int device = -1;
   // scalar (b1) path
@@ -1665,7 +1792,7 @@ struct ThreadCtx {
   size_t stage_cap = 0;
   uint32_t *sout = nullptr;  // page-locked result slot: (tag << 16) | sum
   uint32_t *sout_dev = nullptr;
-  uint32_t stag = 0;         // tag of the last scalar call
+  uint32_t stag = 0;         // tag of the last scalar call (next_tag: 1..0xffff, never 0)
   // host-batch path
   static constexpr int kRing = 3;
   hipStream_t hstream[kRing] = {};
@@ -1701,6 +1828,15 @@ struct ThreadCtx {
   uint32_t nev = 0;
 };
 thread_local ThreadCtx t_ctx;
+// The tag of a thread's next drop-in / burst call: 1..0xffff.  Never 0: a
+// fresh mailbox's sequence word and a fresh result word are 0, so a request
+// tagged 0 (a staged span: no inline chunks, sequence word == tag) would look
+// like no request to a service launched on that mailbox, and its result like
+// one already there.
+uint32_t next_tag(ThreadCtx &c) {
+  c.stag = (c.stag & 0xffffu) == 0xffffu ? 1u : c.stag + 1u;
+  return c.stag;
+}
 
 int check_device(int dev) {
   hipDeviceProp_t prop;
@@ -1722,11 +1858,11 @@ void ctx_release(ThreadCtx &c, int back) {
     }
   };
   auto dfree = [](auto *&p) {
-    if (p) (void)hipFree((void *)p);
+    if (p) (void)jfree((void *)p);
     p = nullptr;
   };
   auto hfree = [](auto *&p) {
-    if (p) (void)hipHostFree((void *)p);
+    if (p) (void)jhostfree((void *)p);
     p = nullptr;
   };
   stream(c.sstream);
@@ -1783,6 +1919,7 @@ int ensure_ctx() {
   }
   t_ctx.device = dev;
   thread_exit_register();
+  fault_reporter_register();
   return 0;
 }
 
@@ -1852,9 +1989,27 @@ int grid_for(uint32_t n, int G) {
   return blocks ? (int)blocks : 1;
 }
 
+// Bytes from p to the end of the allocation that holds it, as the HIP runtime
+// reports it, at most `want` -- the extent a kernel's resource over an array
+// of unknown length gets (the chain / TX segment tables).  `want` when the
+// runtime does not know the pointer (memory from another allocator).
+uint64_t alloc_extent(const void *p, uint64_t want) {
+  if (!p) return 0;
+  hipDeviceptr_t base = nullptr;
+  size_t size = 0;
+  if (hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+    (void)hipGetLastError();  // (not an error of the caller's: clear it)
+    return want;
+  }
+  const uint64_t end = (uint64_t)(uintptr_t)base + size, a = (uint64_t)(uintptr_t)p;
+  return a < end ? std::min<uint64_t>(want, end - a) : 0;
+}
+
 int make_desc(const mi_pkt_batch *b, Desc *d) {
   if (!b) return set_err(-EINVAL, "batch is NULL");
   if (((uintptr_t)b->base & 15u) != 0) return set_err(-EINVAL, "base %p not 16-byte aligned", b->base);
+  // every per-datagram array's byte offset (8 n for u64 offsets) stays 32-bit
+  if (b->n > MI_BATCH_MAX_N) return set_err(-E2BIG, "n %u > MI_BATCH_MAX_N (%u)", b->n, (unsigned)MI_BATCH_MAX_N);
   if (b->bytes > kMaxBytes) return set_err(-E2BIG, "batch buffer %llu B > MI_BATCH_MAX_BYTES (%llu)", (unsigned long long)b->bytes,
                    (unsigned long long)kMaxBytes);
   if (b->n && !b->base) return set_err(-EINVAL, "base is NULL");
@@ -1878,6 +2033,22 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
   d->cflags = nullptr;
   d->cdata = nullptr;
   return 0;
+}
+
+// The journal entries of a launch over a batch (fault reporter): the launch,
+// then the arrays it references with their extents.
+void jdesc(const char *what, uint32_t tag, const Desc &d, const void *ip = nullptr, const void *l4 = nullptr,
+           const void *st = nullptr, const void *bad = nullptr) {
+  jnote(what, nullptr, 0, tag);
+  jnote("  packets", d.base, d.bytes, d.n);
+  if (d.offs) jnote("  offsets", d.offs, (uint64_t)d.n * ((d.flags & MI_BATCH_OFFS32) ? 4u : 8u));
+  if (d.lens) jnote("  lengths", d.lens, 4ull * d.n);
+  if (ip) jnote("  out ip", ip, 2ull * d.n);
+  if (l4) jnote("  out l4", l4, 2ull * d.n);
+  if (st) jnote("  out status", st, d.n);
+  if (bad) jnote("  out bad", bad, 4);
+  if (d.cflags) jnote("  out csum_flags", d.cflags, 4ull * d.n);
+  if (d.cdata) jnote("  out csum_data", d.cdata, 4ull * d.n);
 }
 
 uint32_t batch_max_len(const mi_pkt_batch *b) {
@@ -2053,6 +2224,8 @@ unsigned slot64_blocks(const Desc &d) {
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
                   uint32_t *bad, hipStream_t s) {
   const Plan pl = verify_plan(d, max_len);
+  jdesc("launch verify", (uint32_t)pl.kind * 1000u + (pl.dma ? 100u + pl.dma : pl.run_u * 10u + pl.run_nw), d, ip, l4, st,
+        bad);
   if (pl.kind == kPlanRun && pl.dma) {
 #define X(U_, R_)                                                                                            \
   if (pl.dma == 10 * U_ + R_) {                                                                              \
@@ -2101,6 +2274,10 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
 
 int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd, uint16_t *out,
                 hipStream_t s) {
+  jdesc("launch span", (uint32_t)(sh.g * 100 + sh.u), d, out);
+  if (sd.seeds) jnote("  seeds", sd.seeds, 4ull * d.n);
+  if (sd.src) jnote("  src/dst/proto", sd.src, 4ull * d.n);
+  if (sd.plens) jnote("  plens", sd.plens, 4ull * d.n);
   if ((d.flags & MI_BATCH_PACKED) && !g_tune.g) {  // packed mixed lengths: the flat run
     uint64_t blocks = ((uint64_t)d.n + 255) / 256;
     const int cap = g_tune.max_blocks > 0 ? g_tune.max_blocks : 16384;
@@ -2145,6 +2322,7 @@ bool finalize_blocks_ok(const Desc &d, uint32_t max_len) {
 bool finalize_uses_vlaunch(const Desc &) { return true; }  // every finalize plan is one launch
 
 int launch_finalize(const Desc &d, Shape sh, hipStream_t s, uint32_t max_len) {
+  jdesc("launch finalize", (uint32_t)(sh.g * 100 + sh.u), d);
   // packed mixed lengths and dense slots: the flat-run kernel (as verify_plan
   // picks it for verify), one lane group per datagram otherwise
   const bool dense_slots = !d.offs && !d.lens && d.stride && d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
@@ -2203,6 +2381,14 @@ int tx_kernel_kind() {
 }
 
 int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
+  jnote("launch tx_copy", nullptr, 0, (uint32_t)(sh.g * 100 + sh.u));
+  jnote("  src", t.src, t.src_bytes, t.n);
+  jnote("  dst", t.dst, t.dst_bytes);
+  jnote("  seg_off", t.seg_off, 8ull * t.nseg);
+  jnote("  seg_len", t.seg_len, 4ull * t.nseg);
+  jnote("  pkt_seg", t.pkt_seg, 4ull * t.n + 4);
+  jnote("  pkt_len", t.pkt_len, 4ull * t.n);
+  jnote("  status", t.status, t.n);
   if (tx_kernel_kind() == 2) {
     // one frame per wave: four per workgroup
     hipLaunchKernelGGL((k_tx_wave<2>), dim3(grid_for(t.n, 64)), dim3(kBlock), 0, s, t);
@@ -2423,6 +2609,11 @@ int aql_device(int dev, AqlDevice **out) {
     snprintf(a.err, sizeof a.err, __VA_ARGS__); \
     a.rc = (code);                         \
   } while (0)
+#if MI_DEBUG_BOUNDS
+    // the bounds-report build's kernels call printf, whose buffer is a hidden
+    // argument only a HIP launch fills: every dispatch goes through HIP
+    fail(-ENOTSUP, "the MI_DEBUG_BOUNDS build dispatches through HIP launches only");
+#endif
     // HIP may load a code object lazily: querying the kernels loads it
     for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
       hipFuncAttributes fa;
@@ -2537,6 +2728,7 @@ struct AqlRun {
   hsa_signal_t first{}, rest{};  // pass 0's completion (timing start) / every other pass's
   bool have_first = false, have_rest = false;
   uint8_t *kargs = nullptr;      // device memory: one argument block per batch
+  size_t kargs_bytes = 0;
   std::vector<hsa_kernel_dispatch_packet_t> pkt;  // one prebuilt packet per batch
   uint32_t last_steps = 0;
   bool pending = false;
@@ -2550,9 +2742,25 @@ void aql_free(AqlRun *a) {
   if (a->have_rest) (void)hsa_signal_destroy(a->rest);
   if (a->kargs) {
     dbg_mem("aql-kargs-free", a->kargs, 0);
-    (void)hipFree(a->kargs);
+    jnote("free aql kargs", a->kargs, a->kargs_bytes);
+    (void)jfree(a->kargs);
   }
   delete a;
+}
+// A run whose passes never completed (a fault, a hang, a failed wait): its
+// queues, signals, kernel-argument block and the run object itself (its error
+// slot is the queues' callback data) are kept, not destroyed or freed under
+// dispatches that may still read them -- as aql_one_release does for a
+// thread's queue.  Counted in mi__hsa_queues_leaked, reported on stderr.
+void aql_leak(AqlRun *a) {
+  if (!a) return;
+  int nq = 0;
+  for (hsa_queue_t *q : a->q) nq += q != nullptr;
+  g_live_queues.fetch_sub(nq);
+  g_leaked_queues.fetch_add(nq);
+  jnote("leak aql run", a->kargs, a->kargs_bytes, (uint32_t)nq);
+  fprintf(stderr, "libmicksum: AQL engine passes never completed (%s); the run's %d queue(s), signals and kernel "
+          "arguments are leaked, not freed\n", t_err, nq);
 }
 
 // One kernel-argument block: the explicit arguments, then the code object v5
@@ -2625,8 +2833,10 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
   }
   std::vector<uint8_t> host((size_t)slot * nb, 0);
   a->pkt.resize(nb);
-  hipError_t e = hipMalloc((void **)&a->kargs, host.size());
+  hipError_t e = jmalloc((void **)&a->kargs, host.size());
   dbg_mem("aql-kargs", a->kargs, host.size());
+  a->kargs_bytes = host.size();
+  jnote("aql kargs", a->kargs, host.size(), nb);
   if (e != hipSuccess) {
     aql_free(a);
     return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
@@ -2636,6 +2846,7 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
                   AqlArgs{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr}, blocks[j],
                   aql_wg(ids[j]));
     aql_fill_packet(a->pkt[j], dv->k[ids[j]], blocks[j], a->kargs + (size_t)slot * j, aql_wg(ids[j]));
+    jdesc("  aql batch", (uint32_t)ids[j], d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr);
   }
   e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
@@ -2664,8 +2875,13 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
 }
 
 // Wait for every pass of the last submission (spinning: the RX loop polls).
+thread_local bool t_aql_fail_wait = false;  // mi__aql_fail_next_wait (tests of the leak path)
 int aql_wait(AqlRun *a) {
   if (!a->pending) return 0;
+  if (t_aql_fail_wait) {
+    t_aql_fail_wait = false;
+    return set_err(-ETIMEDOUT, "AQL engine: wait failed (injected by mi__aql_fail_next_wait)");
+  }
   const double t0 = mono_s();
   for (hsa_signal_t s : {a->first, a->rest}) {
     for (;;) {
@@ -2683,6 +2899,7 @@ int aql_wait(AqlRun *a) {
 // Submit `steps` passes starting with batch j0.
 int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
   if (!steps) return 0;
+  jnote("launch aql run", a->kargs, a->kargs_bytes, steps);
   const uint32_t nb = (uint32_t)a->pkt.size();
   hsa_signal_store_relaxed(a->first, 1);
   hsa_signal_store_relaxed(a->rest, (hsa_signal_value_t)(steps - 1));
@@ -2797,6 +3014,7 @@ struct AqlOne {
   uint32_t *mbox = nullptr;
   bool mbox_dev = false;
   uint32_t mbox_seq = 0;
+  bool svc_owner = false;              // holds one of the process's service slots (svc_allowed)
   uint32_t svc_token = 0;              // the running service's launch token
   volatile uint32_t *svc_out = nullptr;  // its result block (host): [6] = token on exit
   bool svc_registered = false;         // in g_svc_reg (the process-exit handler's list)
@@ -2900,6 +3118,7 @@ int aql_one_quiesce(AqlOne &o) {
 std::mutex g_svc_mu;
 std::vector<AqlOne *> g_svc_reg;
 std::atomic<uint32_t> g_svc_tokens{0};
+std::atomic<int> g_svc_owners{0};  // threads holding a service slot (svc_allowed)
 void svc_atexit() {
   std::lock_guard<std::mutex> lk(g_svc_mu);
   for (AqlOne *o : g_svc_reg) {
@@ -2908,6 +3127,9 @@ void svc_atexit() {
     const double t0 = mono_s();
     while (o->svc_out[6] != o->svc_token && mono_s() - t0 < 0.2) {
     }
+    if (o->svc_out[6] != o->svc_token)
+      fprintf(stderr, "libmicksum: at exit, a drop-in service did not stop within 200 ms (a thread still "
+              "inside a drop-in call when exit() ran is not supported)\n");
     o->svc_live = false;
   }
 }
@@ -2931,12 +3153,16 @@ void mbox_free(AqlDevice *a, uint32_t *m);
 bool aql_one_release(AqlOne &o) {
   bool leaked = false;
   svc_unregister(o);
+  if (o.svc_owner) {
+    g_svc_owners.fetch_sub(1);
+    o.svc_owner = false;
+  }
   if (o.q) {
     if (aql_one_quiesce(o) == 0) {
       aql_queue_destroy(o.q);
       if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
       dbg_mem("one-karg-free", o.karg, 0);
-      if (o.karg) (void)hipHostFree(o.karg);
+      if (o.karg) (void)jhostfree(o.karg);
       if (o.mbox && o.mbox_dev) mbox_free(o.dev, o.mbox);
       delete o.err;
     } else {
@@ -3087,7 +3313,7 @@ int aql_one_open(AqlOne &o) {
       aql_one_release(o);
       return set_err(-EIO, "AQL engine: hsa_signal_create failed");
     }
-    if (hipHostMalloc((void **)&o.karg, 512 * kAqlOneSlots, hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (jhostmalloc((void **)&o.karg, 512 * kAqlOneSlots, hipHostMallocMapped | hipHostMallocCoherent) !=
         hipSuccess) {
       o.karg = nullptr;
       aql_one_release(o);
@@ -3149,6 +3375,15 @@ int mi_cksum_hsa_queues(void) { return g_live_queues.load(); }
 // Diagnostics (not in the public header): queues leaked because a dispatch on
 // them never retired (aql_one_release).
 int mi__hsa_queues_leaked(void) { return g_leaked_queues.load(); }
+// Tests of the leak path: the calling thread's next AQL-engine wait fails as
+// a timeout would (the passes are left running; the handle must not free what
+// they use).
+void mi__aql_fail_next_wait(void) { t_aql_fail_wait = true; }
+// The GPU memory-fault reporter: 1 registered with the HSA runtime, -1 the
+// runtime refused a second system-event handler, 0 not tried yet (no GPU).
+int mi__fault_reporter(void) { return g_fault_handler.load(); }
+// Diagnostics: number of journal events recorded so far.
+unsigned long long mi__journal_events(void) { return (unsigned long long)g_jseq.load(); }
 // Diagnostics / tests (not in the public header): waves per workgroup of the
 // flat-run verify kernel (1, 2, 4; speed only, never results).
 int mi__set_run_waves(int w) {
@@ -3218,6 +3453,7 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream) {
   if (b->mode == MI_CHAIN_PSEUDO && (!b->src || !b->dst || !b->proto))
     return set_err(-EINVAL, "pseudo mode needs src / dst / proto");
   if (b->mode != MI_CHAIN_SKIP && b->mode != MI_CHAIN_PSEUDO) return set_err(-EINVAL, "mode");
+  if (b->n > MI_BATCH_MAX_N) return set_err(-E2BIG, "n %u > MI_BATCH_MAX_N", b->n);
   ChainDesc cd{};
   cd.base = (const uint8_t *)b->base;
   cd.bytes = (uint32_t)((b->bytes + 15u) & ~15ull);
@@ -3231,9 +3467,20 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream) {
   cd.dst = b->dst;
   cd.proto = b->proto;
   cd.pseudo = b->mode == MI_CHAIN_PSEUDO;
+  // the segment tables' extent: as given (0: unknown), and never past what
+  // their allocations hold
+  const uint64_t given = b->nseg ? b->nseg : kOOB / 8u;
+  cd.nseg = (uint32_t)std::min({given, alloc_extent(b->seg_off, 8u * given) / 8u,
+                                alloc_extent(b->seg_len, 4u * given) / 4u});
   const Shape sh = pick_shape(b->max_seg ? b->max_seg : 2048u);
   const int grid = grid_for(cd.n, sh.g);
   hipStream_t st = (hipStream_t)stream;
+  jnote("launch chain", nullptr, 0, (uint32_t)(sh.g * 100 + sh.u));
+  jnote("  buffer", cd.base, cd.bytes, cd.n);
+  jnote("  seg_off", cd.seg_off, 8ull * cd.nseg);
+  jnote("  seg_len", cd.seg_len, 4ull * cd.nseg);
+  jnote("  pkt_seg", cd.pkt_seg, 4ull * cd.n + 4);
+  jnote("  out", out, 2ull * cd.n);
 #define X(G_, U_)                                                                              \
   if (sh.g == G_ && sh.u == U_) {                                                              \
     hipLaunchKernelGGL((k_chain<G_, U_>), dim3(grid), dim3(kBlock), 0, st, cd, out);            \
@@ -3295,6 +3542,7 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
     a.e[k].l4 = l4 ? l4[k] : nullptr;
     a.e[k].st = status ? status[k] : nullptr;
     a.e[k].unit0 = units;
+    jdesc(k ? "  multi batch" : "launch verify_multi", k, d[k], a.e[k].ip, a.e[k].l4, a.e[k].st, bad_count);
     const uint64_t u = ((uint64_t)d[k].n + gpw - 1) / gpw;
     if (units + u > 0xffffffffull) return set_err(-E2BIG, "too many datagrams in one launch");
     units += (uint32_t)u;
@@ -3542,10 +3790,10 @@ void repeat_free(mi_repeat *r) {
     if (r->s[q]) (void)hipStreamDestroy(r->s[q]);
   }
   if (r->ev0) (void)hipEventDestroy(r->ev0);
-  if (r->flag) (void)hipHostFree(r->flag);
+  if (r->flag) (void)jhostfree(r->flag);
   if (r->aql) {
-    (void)aql_wait(r->aql);
-    aql_free(r->aql);
+    if (aql_wait(r->aql) == 0) aql_free(r->aql);
+    else aql_leak(r->aql);
   }
   delete r;
 }
@@ -3625,7 +3873,7 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
   }
   if (e == hipSuccess) e = hipEventCreate(&r->ev0);
   if (e == hipSuccess && repeat_wait_mode() == kWaitFlag) {
-    e = hipHostMalloc((void **)&r->flag, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
+    e = jhostmalloc((void **)&r->flag, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&r->flag_dev, r->flag, 0);
     if (e == hipSuccess) memset(r->flag, 0, 64 * sizeof(uint32_t));
   }
@@ -3802,13 +4050,16 @@ int mi_cksum_set_busy_wait(int on) {
 namespace {
 // mi_tx_batch -> kernel descriptor, with the ABI's checks (pointers as given:
 // device pointers, or device views of host memory)
-int make_txdesc(const mi_tx_batch *b, uint8_t *status, TxDesc *out) {
+// nseg: entries of the segment tables when the caller knows it (the host
+// entry points copy them), else -1: the allocations holding them bound it.
+int make_txdesc(const mi_tx_batch *b, uint8_t *status, TxDesc *out, int64_t nseg = -1) {
   if (!b->src || !b->dst || !b->seg_off || !b->seg_len || !b->pkt_seg || !b->pkt_len || !status)
     return set_err(-EINVAL, "NULL array");
   if (((uintptr_t)b->src & 15u) || ((uintptr_t)b->dst & 15u))
     return set_err(-EINVAL, "src / dst not 16-byte aligned");
   if (b->src_bytes > kMaxBytes || b->dst_bytes > kMaxBytes) return set_err(-E2BIG, "buffer > MI_BATCH_MAX_BYTES");
   if (b->l3_off > 64) return set_err(-EINVAL, "l3_off %u > 64", b->l3_off);
+  if (b->n > MI_BATCH_MAX_N) return set_err(-E2BIG, "n %u > MI_BATCH_MAX_N", b->n);
   const uint64_t last = b->dst_first + (uint64_t)(b->n - 1) * b->dst_stride + b->room;
   if (last > b->dst_bytes)
     return set_err(-ERANGE, "slot %u ends at %llu > dst_bytes %llu", b->n - 1, (unsigned long long)last,
@@ -3831,6 +4082,9 @@ int make_txdesc(const mi_tx_batch *b, uint8_t *status, TxDesc *out) {
   t.dst_stride = b->dst_stride;
   t.dst_first = b->dst_first;
   t.status = status;
+  const uint64_t given = nseg >= 0 ? std::min<uint64_t>((uint64_t)nseg, kOOB / 8u) : kOOB / 8u;
+  t.nseg = (uint32_t)std::min({given, alloc_extent(b->seg_off, 8u * given) / 8u,
+                               alloc_extent(b->seg_len, 4u * given) / 4u});
   return 0;
 }
 }  // namespace
@@ -3864,6 +4118,7 @@ int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
   if ((rc = make_desc(b, &d))) return rc;
   hipStream_t st = (hipStream_t)stream;
   d.bytes = (uint32_t)b->bytes;  // header writes stay inside the real buffer
+  jdesc("launch synth", 0, d);
   const uint64_t fill = b->bytes & ~15ull;
   if (fill) {
     uint64_t blocks = (fill / 16 + kBlock - 1) / kBlock;
@@ -3899,6 +4154,7 @@ int mi_cksum_host_register(void *p, uint64_t bytes) {
   int rc = ensure_ctx();
   if (rc) return rc;
   HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
+  jnote("host register", p, bytes);
   dbg_mem("host-register", p, bytes);
   // the mapping covers whole pages
   const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + bytes + 4095) & ~(uintptr_t)4095;
@@ -3918,6 +4174,7 @@ int mi_cksum_host_unregister(void *p) {
       }
   }
   dbg_mem("host-unregister", p, 0);
+  jnote("host unregister", p, alloc_bytes(p));
   HIP_TRY(hipHostUnregister(p));
   return 0;
 }
@@ -3929,6 +4186,30 @@ int mi_cksum_host_unregister(void *p) {
 // in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
 // mailbox) against 8.1 us for a dispatch per call.
 std::atomic<int> g_dropin_svc{-1};
+// At most MI_CKSUM_DROPIN_SERVICE_MAX (default 8) threads of the process run
+// a drop-in service at once: each is a resident 512-lane workgroup polling
+// its thread's own HSA queue, and more of them than the hardware maps queues
+// for would be time-sliced by the command processor.  A thread
+// takes a slot with its first service call and gives it back when its queue is
+// released (thread exit, device switch); threads beyond the cap keep one
+// dispatch per call.
+int dropin_svc_max() {
+  static const int m = [] {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_MAX");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 8;
+  }();
+  return m;
+}
+bool svc_allowed(AqlOne &o) {
+  if (o.svc_owner) return true;
+  if (g_svc_owners.fetch_add(1) >= dropin_svc_max()) {
+    g_svc_owners.fetch_sub(1);
+    return false;
+  }
+  o.svc_owner = true;
+  return true;
+}
 bool dropin_svc_on() {
   int v = g_dropin_svc.load(std::memory_order_relaxed);
   if (v < 0) {
@@ -3962,7 +4243,7 @@ static int ensure_sout(ThreadCtx &c) {
   if (c.sout) return 0;
   // words 0..5: the result and the trace stamps; 16..: the service mailbox
   // when it lives in host memory
-  HIP_TRY(hipHostMalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_TRY(jhostmalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
   memset(c.sout, 0, 4096);
   dbg_mem("sout", c.sout_dev, 4096);
@@ -4048,12 +4329,12 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   // (each a queue round trip, ~10 us apiece for a 512-packet burst).
   const size_t need = 25 * n + 128;
   if (c.zhost_cap < need) {
-    if (c.zhost) HIP_TRY(hipHostFree(c.zhost));
+    if (c.zhost) HIP_TRY(jhostfree(c.zhost));
     c.zhost = c.zhost_dev = nullptr;
     c.zhost_cap = 0;
     size_t cap = 1u << 16;
     while (cap < need) cap <<= 1;
-    HIP_TRY(hipHostMalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_TRY(jhostmalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
     HIP_TRY(hipHostGetDevicePointer((void **)&c.zhost_dev, c.zhost, 0));
     dbg_mem("zhost", c.zhost_dev, cap);
     c.zhost_cap = cap;
@@ -4127,7 +4408,7 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     const long v = e ? atol(e) : 64L;
     return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
   }();
-  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0) {
+  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0 && svc_allowed(t_aql1)) {
     AqlOne &o = t_aql1;
     int rc = svc_open(c, o);
     if (rc) return rc;
@@ -4151,8 +4432,7 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     a.st = zst;
     a.bad = nullptr;
     memcpy(inl, &a, sizeof a);
-    c.stag = (c.stag + 1) & 0xffffu;
-    const uint32_t tag = c.stag, prev = o.mbox_seq;
+    const uint32_t tag = next_tag(c), prev = o.mbox_seq;
     if (!o.svc_live && (rc = svc_launch(c, o, prev))) return rc;
     mbox_post(o, 0x40000000u | (((uint32_t)(sizeof a + 15u) >> 4) << 16) | tag);  // bit 30: a burst
     uint32_t w;
@@ -4254,26 +4534,26 @@ static int host_batch(const mi_pkt_batch *b, const HostOut &o, uint32_t *bad_cou
   if (!c.hstream[0])
     for (int k = 0; k < ThreadCtx::kRing; ++k)
       HIP_TRY(hipStreamCreateWithFlags(&c.hstream[k], hipStreamNonBlocking));
-  if (!c.dbad) HIP_TRY(hipMalloc(&c.dbad, 4 * ThreadCtx::kRing));
+  if (!c.dbad) HIP_TRY(jmalloc(&c.dbad, 4 * ThreadCtx::kRing));
   if (c.dstage_cap < need_stage) {
     for (int k = 0; k < ThreadCtx::kRing; ++k) {
-      if (c.dstage[k]) HIP_TRY(hipFree(c.dstage[k]));
-      HIP_TRY(hipMalloc(&c.dstage[k], need_stage));
+      if (c.dstage[k]) HIP_TRY(jfree(c.dstage[k]));
+      HIP_TRY(jmalloc(&c.dstage[k], need_stage));
     }
     c.dstage_cap = need_stage;
   }
   if (c.dout_cap < max_pk) {
     for (int k = 0; k < ThreadCtx::kRing; ++k) {
-      if (c.dout[k]) HIP_TRY(hipFree(c.dout[k]));
-      if (c.dst8[k]) HIP_TRY(hipFree(c.dst8[k]));
-      if (c.ddesc[k]) HIP_TRY(hipFree(c.ddesc[k]));
-      if (c.hdesc[k]) HIP_TRY(hipHostFree(c.hdesc[k]));
-      if (c.dflag[k]) HIP_TRY(hipFree(c.dflag[k]));
-      HIP_TRY(hipMalloc(&c.dflag[k], 8ull * max_pk));
-      HIP_TRY(hipMalloc(&c.dout[k], 4ull * max_pk));
-      HIP_TRY(hipMalloc(&c.dst8[k], (size_t)max_pk + 16));
-      HIP_TRY(hipMalloc(&c.ddesc[k], 12ull * max_pk));
-      HIP_TRY(hipHostMalloc((void **)&c.hdesc[k], 12ull * max_pk, hipHostMallocDefault));
+      if (c.dout[k]) HIP_TRY(jfree(c.dout[k]));
+      if (c.dst8[k]) HIP_TRY(jfree(c.dst8[k]));
+      if (c.ddesc[k]) HIP_TRY(jfree(c.ddesc[k]));
+      if (c.hdesc[k]) HIP_TRY(jhostfree(c.hdesc[k]));
+      if (c.dflag[k]) HIP_TRY(jfree(c.dflag[k]));
+      HIP_TRY(jmalloc(&c.dflag[k], 8ull * max_pk));
+      HIP_TRY(jmalloc(&c.dout[k], 4ull * max_pk));
+      HIP_TRY(jmalloc(&c.dst8[k], (size_t)max_pk + 16));
+      HIP_TRY(jmalloc(&c.ddesc[k], 12ull * max_pk));
+      HIP_TRY(jhostmalloc((void **)&c.hdesc[k], 12ull * max_pk, hipHostMallocDefault));
     }
     c.dout_cap = max_pk;
   }
@@ -4414,12 +4694,12 @@ int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags)
   if (zc) {
     // zero-copy: descriptors and status through the mapped per-thread block
     if (c.zhost_cap < need) {
-      if (c.zhost) HIP_TRY(hipHostFree(c.zhost));
+      if (c.zhost) HIP_TRY(jhostfree(c.zhost));
       c.zhost = c.zhost_dev = nullptr;
       c.zhost_cap = 0;
       size_t cap = 1u << 16;
       while (cap < need) cap <<= 1;
-      HIP_TRY(hipHostMalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
+      HIP_TRY(jhostmalloc((void **)&c.zhost, cap, hipHostMallocMapped | hipHostMallocCoherent));
       HIP_TRY(hipHostGetDevicePointer((void **)&c.zhost_dev, c.zhost, 0));
       c.zhost_cap = cap;
     }
@@ -4427,7 +4707,7 @@ int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags)
     mi_tx_batch v;
     view(c.zhost_dev, sdev, ddev, &v);
     TxDesc t;
-    if ((rc = make_txdesc(&v, c.zhost_dev + o_st, &t))) return rc;
+    if ((rc = make_txdesc(&v, c.zhost_dev + o_st, &t, (int64_t)nseg))) return rc;
     if ((rc = launch_tx(t, sh, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
     memcpy(status, c.zhost + o_st, n);
@@ -4438,10 +4718,10 @@ int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags)
   if (!b->src || !b->dst) return set_err(-EINVAL, "NULL array");
   auto grow = [&](uint8_t *&p, size_t &cap, size_t want) -> int {
     if (cap >= want) return 0;
-    if (p) HIP_TRY(hipFree(p));
+    if (p) HIP_TRY(jfree(p));
     p = nullptr;
     cap = 0;
-    HIP_TRY(hipMalloc((void **)&p, want));
+    HIP_TRY(jmalloc((void **)&p, want));
     cap = want;
     return 0;
   };
@@ -4457,7 +4737,7 @@ int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags)
   mi_tx_batch v;
   view(c.tx_desc, c.tx_src, c.tx_dst, &v);
   TxDesc t;
-  if ((rc = make_txdesc(&v, c.tx_desc + o_st, &t))) return rc;
+  if ((rc = make_txdesc(&v, c.tx_desc + o_st, &t, (int64_t)nseg))) return rc;
   if ((rc = launch_tx(t, sh, st))) return rc;
   HIP_TRY(hipMemcpyAsync(b->dst, c.tx_dst, b->dst_bytes, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipMemcpyAsync(status, c.tx_desc + o_st, n, hipMemcpyDeviceToHost, st));
@@ -4480,16 +4760,16 @@ uint8_t *mi__scalar_staging(size_t need) {
     }
     if (c.stage) {
       dbg_mem("stage-free", c.stage_dev, 0);
-      (void)hipHostFree(c.stage);
+      (void)jhostfree(c.stage);
     }
     c.stage = c.stage_dev = nullptr;
     c.stage_cap = 0;
     size_t cap = 1;
     while (cap < need) cap <<= 1;
-    hipError_t e = hipHostMalloc((void **)&c.stage, cap, hipHostMallocMapped);
+    hipError_t e = jhostmalloc((void **)&c.stage, cap, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c.stage_dev, c.stage, 0);
     if (e != hipSuccess) {
-      set_err(-ENOMEM, "hipHostMalloc(%zu): %s", cap, hipGetErrorString(e));
+      set_err(-ENOMEM, "jhostmalloc(%zu): %s", cap, hipGetErrorString(e));
       return nullptr;
     }
     c.stage_cap = cap;
@@ -4518,8 +4798,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     return set_err(-EINVAL, "scalar staging overrun");
   if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
   if ((rc = ensure_sout(c))) return rc;
-  c.stag = (c.stag + 1) & 0xffffu;
-  const uint32_t tag = c.stag;
+  const uint32_t tag = next_tag(c);
   const bool trace = t_dtrace.on;
   if (trace) memset(c.sout + 2, 0, 16);
   struct ScalarArgs {  // mi_aql_scalar's parameters, in order
@@ -4536,7 +4815,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   }();
   AqlDevice *adv = nullptr;
   const bool aql = host_aql && aql_device(c.device, &adv) == 0;
-  const bool svc = aql && dropin_svc_on();
+  const bool svc = aql && dropin_svc_on() && svc_allowed(t_aql1);
   AqlOne &o = t_aql1;
   uint32_t prev = 0;
   if (svc) {
@@ -4660,6 +4939,10 @@ int mi__set_dropin_service(int on) {
 }
 // Is the calling thread's drop-in service running?  (tests)
 int mi__dropin_service_live(void) { return t_aql1.svc_live ? 1 : 0; }
+// Tests: the calling thread's last drop-in tag (the next call uses the one
+// after it), and the number of threads holding a service slot.
+void mi__set_dropin_tag(uint32_t tag) { t_ctx.stag = tag & 0xffffu; }
+int mi__dropin_service_owners(void) { return g_svc_owners.load(); }
 // Where the calling thread's service mailbox lives: 0 none yet, 1 page-locked
 // host memory, 2 device memory written through the BAR.  (tests, bench)
 int mi__dropin_mailbox(void) { return !t_aql1.mbox ? 0 : t_aql1.mbox_dev ? 2 : 1; }

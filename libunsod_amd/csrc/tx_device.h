@@ -43,7 +43,18 @@ struct TxDesc {
   uint32_t room, l3;
   uint64_t dst_stride, dst_first;
   uint8_t *status;
+  uint32_t nseg;  // segments the seg_off / seg_len tables hold (host: their allocation)
 };
+// The TX batch's tables as bounded arrays (cksum_device.h, Arr).
+struct TxArrs {
+  Arr pkt_len, pkt_seg, seg_len, seg_off, cflags, cdata, status;
+};
+__device__ __forceinline__ TxArrs tx_arrs(const TxDesc &t) {
+  const uint64_t n = t.n;
+  return {arr_of(t.pkt_len, 4u * n),          arr_of(t.pkt_seg, 4u * (n + 1u)), arr_of(t.seg_len, 4ull * t.nseg),
+          arr_of(t.seg_off, 8ull * t.nseg),   arr_of(t.cflags, 4u * n),        arr_of(t.cdata, 4u * n),
+          arr_of(t.status, n)};
+}
 
 // The 16 bytes at source address a (any alignment): the aligned chunk at
 // a & ~15 and (unless aligned) the next one, funnel-shifted.
@@ -342,12 +353,13 @@ __device__ __forceinline__ TxPlan tx_plan(const TxDesc &t, uint32_t i, uint32_t 
   TxPlan pl;
   const uint32_t flen = len >= t.l3 ? len - t.l3 : 0u;
   pl.ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen && ih.iplen >= ih.hl && ih.iplen <= flen;
+  const TxArrs ta = tx_arrs(t);
   const uint32_t fl =
-      t.cflags ? t.cflags[i] : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
+      t.cflags ? ld_u32(ta.cflags, i) : MI_CSUM_IP | (ih.proto == 6u ? MI_CSUM_TCP : ih.proto == 17u ? MI_CSUM_UDP : 0u);
   pl.do_ip = pl.ok && (fl & MI_CSUM_IP);
   pl.do_l4 = pl.ok && (fl & (MI_CSUM_TCP | MI_CSUM_UDP));
   pl.udp = fl & MI_CSUM_UDP;
-  pl.at = ih.hl + (t.cdata ? t.cdata[i] : (fl & MI_CSUM_TCP) ? MI_CSUM_DATA_TCP : MI_CSUM_DATA_UDP);
+  pl.at = ih.hl + (t.cdata ? ld_u32(ta.cdata, i) : (fl & MI_CSUM_TCP) ? MI_CSUM_DATA_TCP : MI_CSUM_DATA_UDP);
   pl.hend = pl.ok ? (int)ih.hl : 0;
   pl.lend = pl.ok ? (int)ih.iplen : 0;
   return pl;
@@ -366,6 +378,7 @@ __device__ __forceinline__ uint8_t tx_status(const TxPlan &pl, bool l4_store) {
 template <int G, int U>
 __device__ __forceinline__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffer_rsrc_t rs, __amdgpu_buffer_rsrc_t rd, uint32_t i,
                                  int lane, uint32_t len, uint32_t k0, uint32_t k1, uint32_t ip_mlen) {
+  const TxArrs ta = tx_arrs(t);
   const uint32_t l3 = t.l3;
   const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
   const uint32_t h = D & 15u, c0 = D & ~15u;
@@ -383,10 +396,10 @@ __device__ __forceinline__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffe
       v[u] = u32x4{0, 0, 0, 0};
       int pos = 0;
       for (uint32_t k = k0; k < k1; ++k) {
-        const int l = max(t.seg_len[k], 0);
+        const int l = max((int32_t)ld_u32(ta.seg_len, k), 0);
         const int lo = max(pos - cs, 0), hi = min(min(pos + l, (int)len) - cs, 16);
         if (hi > lo) {
-          const uint32_t a = (uint32_t)cs + ((uint32_t)t.seg_off[k] - (uint32_t)pos);
+          const uint32_t a = (uint32_t)cs + ((uint32_t)ld_u64(ta.seg_off, k) - (uint32_t)pos);
           merge_bytes(v[u], shift_pair(ld_pair(rs, a), a), lo, hi);
         }
         pos += l;
@@ -423,7 +436,7 @@ __device__ __forceinline__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffe
       }
     }
   }
-  if (lane == 0) t.status[i] = tx_status(pl, l4_store);
+  if (lane == 0) st_u8(ta.status, i, tx_status(pl, l4_store));
 }
 
 // U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
@@ -440,6 +453,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
   dd.base = t.dst;
   dd.bytes = t.dst_bytes;
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
+  const TxArrs ta = tx_arrs(t);
   const int lane = threadIdx.x & (G - 1);
   const uint32_t grp = (threadIdx.x & 255u) / G;
   const uint32_t stride = gridDim.x * (kBlock / G);
@@ -454,12 +468,12 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
   int32_t sl_c = 0;
   uint32_t so_c = 0;
   if (i < t.n) {
-    len_c = t.pkt_len[i];
-    k0_c = t.pkt_seg[i];
-    k1_c = t.pkt_seg[i + 1];
+    len_c = ld_u32(ta.pkt_len, i);
+    k0_c = ld_u32(ta.pkt_seg, i);
+    k1_c = ld_u32(ta.pkt_seg, i + 1);
     if (k0_c + lane < k1_c) {
-      sl_c = t.seg_len[k0_c + lane];
-      so_c = (uint32_t)t.seg_off[k0_c + lane];
+      sl_c = (int32_t)ld_u32(ta.seg_len, k0_c + lane);
+      so_c = (uint32_t)ld_u64(ta.seg_off, k0_c + lane);
     }
   }
   for (; i < t.n; i += stride) {
@@ -470,9 +484,9 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
     const uint32_t in = i + stride;
     uint32_t len_n = 0, k0_n = 0, k1_n = 0;
     if (in < t.n) {
-      len_n = t.pkt_len[in];
-      k0_n = t.pkt_seg[in];
-      k1_n = t.pkt_seg[in + 1];
+      len_n = ld_u32(ta.pkt_len, in);
+      k0_n = ld_u32(ta.pkt_seg, in);
+      k1_n = ld_u32(ta.pkt_seg, in + 1);
     }
     bool pre2 = false;
     auto prefetch2 = [&]() {
@@ -481,8 +495,8 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       sl_c = 0;
       so_c = 0;
       if (in < t.n && k0_n + lane < k1_n) {
-        sl_c = t.seg_len[k0_n + lane];
-        so_c = (uint32_t)t.seg_off[k0_n + lane];
+        sl_c = (int32_t)ld_u32(ta.seg_len, k0_n + lane);
+        so_c = (uint32_t)ld_u64(ta.seg_off, k0_n + lane);
       }
       len_c = len_n;
       k0_c = k0_n;
@@ -498,7 +512,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
     uint32_t total = 0, ip_mlen = 0, m = 0;
     for (uint32_t w = k0; w < k1 && !st; w += G) {
       const uint32_t k = w + lane;
-      const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : t.seg_len[k], 0) : 0u;
+      const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : (int32_t)ld_u32(ta.seg_len, k), 0) : 0u;
       const uint32_t inc = group_scan<G>(l);
       const uint32_t a = total + inc - l, e = total + inc;
       const uint32_t nz = l ? 1u : 0u;
@@ -506,7 +520,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       const uint32_t idx = m + zi - nz;
       if (nz && idx < (uint32_t)kTxSeg) {
         s_seg[grp][idx][0] = a;
-        s_seg[grp][idx][1] = (w == k0 ? so0 : (uint32_t)t.seg_off[k]) - a;
+        s_seg[grp][idx][1] = (w == k0 ? so0 : (uint32_t)ld_u64(ta.seg_off, k)) - a;
       }
       const bool isip = l && a <= l3 && l3 < e;
       ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
     }
     if (!st && total < len) st = MI_TX_SHORT;
     if (st) {
-      if (lane == 0) t.status[i] = (uint8_t)st;
+      if (lane == 0) st_u8(ta.status, i, st);
       prefetch2();
       continue;
     }
@@ -620,8 +634,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         const uint32_t ci = lane;
         const int cs = (int)(16u * ci) - (int)h;
         if (ci < nch) store_chunk(rd, c0 + 16u * ci, held, -cs, (int)len - cs);
-        if (lane == 0)
-          t.status[i] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+        if (lane == 0) st_u8(ta.status, i, (ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
       }
       __builtin_amdgcn_wave_barrier();  // s_seg is rewritten by the group's next frame
     }
@@ -703,6 +716,7 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
   dd.base = t.dst;
   dd.bytes = t.dst_bytes;
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
+  const TxArrs ta = tx_arrs(t);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * (kBlock / 64);
   const uint32_t lim = t.src_bytes - 16u;
@@ -713,12 +727,12 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
   int32_t sl_c = 0;
   uint32_t so_c = 0;
   if (f < t.n) {
-    len_c = t.pkt_len[f];
-    k0_c = t.pkt_seg[f];
-    k1_c = t.pkt_seg[f + 1];
+    len_c = ld_u32(ta.pkt_len, f);
+    k0_c = ld_u32(ta.pkt_seg, f);
+    k1_c = ld_u32(ta.pkt_seg, f + 1);
     if (k0_c + lane < k1_c) {
-      sl_c = t.seg_len[k0_c + lane];
-      so_c = (uint32_t)t.seg_off[k0_c + lane];
+      sl_c = (int32_t)ld_u32(ta.seg_len, k0_c + lane);
+      so_c = (uint32_t)ld_u64(ta.seg_off, k0_c + lane);
     }
   }
   for (; f < t.n; f += nw) {
@@ -729,9 +743,9 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
     const uint32_t fn = f + nw;
     uint32_t len_n = 0, k0_n = 0, k1_n = 0;
     if (fn < t.n) {
-      len_n = t.pkt_len[fn];
-      k0_n = t.pkt_seg[fn];
-      k1_n = t.pkt_seg[fn + 1];
+      len_n = ld_u32(ta.pkt_len, fn);
+      k0_n = ld_u32(ta.pkt_seg, fn);
+      k1_n = ld_u32(ta.pkt_seg, fn + 1);
     }
     bool pre2 = false;
     auto prefetch2 = [&]() {
@@ -740,8 +754,8 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
       sl_c = 0;
       so_c = 0;
       if (fn < t.n && k0_n + lane < k1_n) {
-        sl_c = t.seg_len[k0_n + lane];
-        so_c = (uint32_t)t.seg_off[k0_n + lane];
+        sl_c = (int32_t)ld_u32(ta.seg_len, k0_n + lane);
+        so_c = (uint32_t)ld_u64(ta.seg_off, k0_n + lane);
       }
       len_c = len_n;
       k0_c = k0_n;
@@ -760,7 +774,7 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
       uint32_t total = 0;
       for (uint32_t w = k0; w < k1; w += 64u) {
         const uint32_t k = w + lane;
-        const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : t.seg_len[k], 0) : 0u;
+        const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : (int32_t)ld_u32(ta.seg_len, k), 0) : 0u;
         const uint32_t inc = wave_scan(l);
         const uint32_t a = total + inc - l, e = total + inc;
         const uint64_t ipb = __ballot(l != 0u && a <= l3 && l3 < e);
@@ -935,14 +949,14 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
           if (pl4 < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)c_l4, rd, D + pl4, 0, 0);
           if (pl4 + 1u < len) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(c_l4 >> 8), rd, D + pl4 + 1u, 0, 0);
         }
-        if (lane == 0) t.status[f] = (uint8_t)((ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+        if (lane == 0) st_u8(ta.status, f, (ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
         done = true;
         __builtin_amdgcn_wave_barrier();  // the cells are rewritten for the wave's next frame
         }
       }
     }
     if (st) {
-      if (lane == 0) t.status[f] = (uint8_t)st;
+      if (lane == 0) st_u8(ta.status, f, st);
       done = true;
     }
     prefetch2();
