@@ -166,6 +166,17 @@ def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev
 POISON = {"ip": -1, "l4": -1, "status": 0xFF}  # no verdict of a verify pass: status bits are 1/2/4/8
 
 
+def repeat_plan(b) -> str:
+    """The verify kernel the prepared submission runs for batch b (the
+    dealt-unit kernel where it applies, mi__repeat_plan)."""
+    import ctypes as C
+    import libunsod_amd as mi
+    f = mi.load().mi__repeat_plan
+    f.restype = C.c_char_p
+    f.argtypes = [C.c_void_p]
+    return f(C.byref(b.c)).decode()
+
+
 def poison_outputs(outs) -> None:
     for o in outs:
         for k, t in o.items():
@@ -328,8 +339,8 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
             break
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic, traffic_source=tsrc,
-                kernel=mi.verify_plan(batches[0]) + (" (its AQL entry point mi_aql_*)" if rep is not None and
-                                                     getattr(rep, "engine", "hip") == "aql" else ""),
+                kernel=repeat_plan(batches[0]) + (" (its AQL entry point mi_aql_*)" if rep is not None and
+                                                  getattr(rep, "engine", "hip") == "aql" else ""),
                 alg_bytes_per_launch=int(alg_bytes),
                 avg_launch_us=round(gpu_s_per_launch * 1e6, 2), streams=nst,
                 wall_frac=round(alg_bytes * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))

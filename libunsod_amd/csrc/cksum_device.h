@@ -755,6 +755,81 @@ __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uin
   }
 }
 
+// RX verify with DEALT units (round 5, VERDICT r4 "do this" 5): one launch in
+// flight -- the reference's single RX kthread on one queue -- ends with a
+// second, partial generation of waves (a 2048-workgroup grid is 8192 waves for
+// 5120 slots: a 10.5 us tail).  Here the grid is ONE resident
+// generation.  A unit is one wave's 64 / G datagrams; wave w takes unit w,
+// then deals itself further units from one of kDealCtrs counters (counter c
+// serves the workgroups b with b % kDealCtrs == c, and deals slice c of the
+// units past the first generation's), so every wave stays busy until the
+// units run out and the launch ends within about one unit of its steady rate.
+// Why this shape (tools/xcd_probe.hip, profiles/r05/xcd_probe_r05.jsonl):
+// same-address atomics serialize at ~66 per us whatever their scope, so one
+// counter per launch (or per XCD) would be the bottleneck and a first grab by
+// every wave at once would queue for ~10 us; with the first unit static and 64
+// counters each sees ~250 grabs per 1500 B launch, spread over it.  The next
+// ticket is fetched while the current unit is folded.  A set of counters must
+// not be shared by launches in flight together: the prepared submissions own
+// one set per stream / queue, and a launch leaves its counters at 0 -- each
+// counter is taken exactly units_c + waves_c times (every wave ends with one
+// failing grab), and the wave that draws the last ticket resets it.
+constexpr uint32_t kDealCtrs = 64;                 // counters per set, 64 bytes apart
+constexpr uint32_t kDealSetBytes = kDealCtrs * 64u;
+struct NoHook {
+  __device__ __forceinline__ void operator()() const {}
+};
+// (hook: called after each unit -- tools/timeline.hip stamps the waves)
+template <int G, int U, typename Hook = NoHook>
+__device__ __forceinline__ void verify_dyn_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                                uint32_t *bad, uint32_t *deal, Hook hook = Hook()) {
+  constexpr uint32_t gpw = 64u / G, wpb = kBlock / 64;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t lane64 = threadIdx.x & 63u, gid = lane64 / G;
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * wpb;
+  const uint32_t T = (d.n + gpw - 1) / gpw;  // units
+  const uint32_t c = blockIdx.x % kDealCtrs;
+  // counter c deals units nw + c, nw + c + kDealCtrs, ...: the counters
+  // advance together, so the waves keep sweeping ONE window of the batch in
+  // order (units dealt from kDealCtrs separate slices -- that many regions
+  // read at once -- measured 1-2 us slower per launch)
+  const uint32_t s0 = nw + c, sc = s0 < T ? (T - s0 + kDealCtrs - 1) / kDealCtrs : 0u;
+  const uint32_t nb_c = gridDim.x / kDealCtrs + (c < gridDim.x % kDealCtrs ? 1u : 0u);
+  const uint32_t last = sc + nb_c * wpb - 1u;  // the counter's last ticket this launch
+  const Arr ctr = arr_of(deal, kDealSetBytes);
+  auto grab = [&]() -> uint32_t {
+    uint32_t t = 0;
+    if (lane64 == 0) t = (uint32_t)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, ctr.r, (int)(64u * c), 0, 0);
+    return t;
+  };
+  uint32_t u = blockIdx.x * wpb + wv;  // the static first unit
+  uint32_t t = grab();                 // the next ticket, in flight
+  for (;;) {
+    const uint32_t i = u * gpw + gid;
+    if (u < T && i < d.n) {
+      const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+      u32x4 v[U];
+      issue_first<G, U>(r, off, flen, lane, v);
+      IpHdr ih;
+      bool hdr_ok, l4_ok;
+      uint32_t sum_h, sum_l;
+      ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+      if (lane == 0)
+        verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
+                    ip_out, l4_out, st_out, bad, d);
+    }
+    hook();
+    const uint32_t tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+    if (tk >= sc) {
+      if (tk == last && lane64 == 0) st_u32(ctr, 16u * c, 0u);  // every other grab of this launch is done
+      break;
+    }
+    u = s0 + tk * kDealCtrs;
+    t = grab();
+  }
+}
 // The kernel-argument table of a multi-batch launch (k_ipv4_verify_multi):
 // up to kMaxMulti batches with their outputs.
 constexpr int kMaxMulti = 16;

@@ -84,6 +84,12 @@ __device__ __forceinline__ void verify_body(const Desc &d, uint16_t *ip_out, uin
   });
   if (lane == 0) verify_emit(pend, ip_out, l4_out, st_out, bad, d);
 }
+// RX verify with dealt units: verify_dyn_body (cksum_device.h).
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void k_ipv4_verify_dyn(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                                             uint32_t *bad, uint32_t *deal) {
+  verify_dyn_body<G, U>(d, ip_out, l4_out, st_out, bad, deal);
+}
 // (Holding the U <= 6 shapes to 6 waves per SIMD -- 16x6 at 80 VGPRs instead
 // of 91 -- was built and measured: the 2-queue headline unchanged, 14.16-14.31
 // vs 14.16-14.31 us per pass over 400 steps; one stream 18.4-18.7 vs 18.4-20.0;
@@ -1387,6 +1393,15 @@ constexpr int kScalarThreads = 512;
   }
 #define MI_AQL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12) X(64, 4)
 MI_AQL_SHAPES(MI_AQL_SHAPE)
+// (the dealt-unit verify, k_ipv4_verify_dyn: mi_aql_vd_<G>x<U>, one more
+// argument -- the queue's counter set -- for pick_shape's shapes)
+#define MI_DEAL_SHAPES(X) X(1, 4) X(1, 8) X(4, 4) X(8, 4) X(16, 6) X(8, 8) X(8, 12)
+#define MI_AQL_DEAL(G_, U_)                                                                             \
+  extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_vd_##G_##x##U_(                            \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad, uint32_t *deal) {                 \
+    verify_dyn_body<G_, U_>(d, ip, l4, st, bad, deal);                                                  \
+  }
+MI_DEAL_SHAPES(MI_AQL_DEAL)
 // (the flat run with 1- and 2-wave workgroups: mi_aql_run<U>w<NW>)
 #define MI_AQL_RUN_W(U_, NW_)                                                                           \
   extern "C" __global__ __launch_bounds__(64 * NW_) void mi_aql_run##U_##w##NW_(                        \
@@ -1826,6 +1841,7 @@ struct ThreadCtx {
   hipEvent_t rfork = nullptr, rjoin[kMaxRep] = {};
   hipEvent_t *ev = nullptr;
   uint32_t nev = 0;
+  uint32_t *rdeal = nullptr;  // dealt-unit counter sets, one per repeat stream (kMaxRep x kDealSetBytes)
 };
 thread_local ThreadCtx t_ctx;
 // The tag of a thread's next drop-in / burst call: 1..0xffff.  Never 0: a
@@ -1882,6 +1898,7 @@ void ctx_release(ThreadCtx &c, int back) {
   dfree(c.tx_src);
   dfree(c.tx_dst);
   dfree(c.tx_desc);
+  dfree(c.rdeal);
   for (int q = 0; q < ThreadCtx::kMaxRep; ++q) {
     stream(c.rstream[q]);
     if (c.rjoin[q]) (void)hipEventDestroy(c.rjoin[q]);
@@ -2221,9 +2238,79 @@ unsigned slot64_blocks(const Desc &d) {
   return blocks ? (unsigned)blocks : 1u;
 }
 
+// Dealt units (verify_dyn_body) for the prepared submissions, which own a
+// counter set per stream / queue: lane-group plans whose units outnumber one
+// resident generation.  OFF by default -- measured slower on MI355X, same
+// box, same command (profiles/r05/deal_ab_r05.jsonl): 1500 B two queues 16.3-
+// 16.9 us per launch against 14.8 static (the resident grid holds the machine
+// until its pool is empty, so the next launch cannot ramp under its drain),
+// one launch in flight 23.1-23.4 against 21.7 -- DESIGN.md 5.6.
+// MI_CKSUM_DEAL=1 (or mi__set_deal) turns it on.
+std::atomic<int> g_deal{-1};
+bool deal_on() {
+  int v = g_deal.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_DEAL");
+    v = e && e[0] == '1' ? 1 : 0;
+    g_deal.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+// One resident generation of kernel fn on the calling thread's device (256-
+// thread workgroups): its occupancy in workgroups per CU times the CU count
+// (cached per kernel and device).
+unsigned resident_blocks(const void *fn) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void *, int>, unsigned>> cache;
+  const int dev = t_ctx.device;
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto &e : cache)
+    if (e.first.first == fn && e.first.second == dev) return e.second;
+  int per_cu = 0, cus = 0;
+  unsigned r = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, 0) == hipSuccess && per_cu > 0 &&
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0)
+    r = (unsigned)(per_cu * cus);
+  (void)hipGetLastError();
+  cache.push_back({{fn, dev}, r});
+  return r;
+}
+// The dealt-unit kernel of shape sh for d, and its grid (one resident
+// generation), or false when the static grid is the better plan.
+template <typename F>
+bool deal_plan(const Desc &d, Shape sh, F fn_of, const void **fn, unsigned *blocks) {
+  if (!deal_on() || g_tune.max_blocks > 0) return false;
+  *fn = fn_of(sh);
+  if (!*fn) return false;
+  const unsigned res = resident_blocks(*fn);
+  const uint64_t units = ((uint64_t)d.n + 64u / sh.g - 1) / (64u / sh.g);
+  if (!res || units <= 4ull * res) return false;
+  *blocks = res;
+  return true;
+}
+const void *deal_kernel(Shape sh) {
+#define X(G_, U_) if (sh.g == G_ && sh.u == U_) return (const void *)k_ipv4_verify_dyn<G_, U_>;
+  MI_DEAL_SHAPES(X)
+#undef X
+  return nullptr;
+}
+
 int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, uint8_t *st,
-                  uint32_t *bad, hipStream_t s) {
+                  uint32_t *bad, hipStream_t s, uint32_t *deal = nullptr) {
   const Plan pl = verify_plan(d, max_len);
+  const void *dfn = nullptr;
+  unsigned dblocks = 0;
+  if (deal && pl.kind == kPlanShape && deal_plan(d, pl.shape, deal_kernel, &dfn, &dblocks)) {
+    jdesc("launch verify (dealt units)", (uint32_t)(pl.shape.g * 100 + pl.shape.u), d, ip, l4, st, bad);
+    jnote("  deal counters", deal, kDealSetBytes, dblocks);
+#define X(G_, U_)                                                                                              \
+  if (pl.shape.g == G_ && pl.shape.u == U_) {                                                                  \
+    VLAUNCH((k_ipv4_verify_dyn<G_, U_>), dim3(dblocks), dim3(kBlock), 0, s, d, ip, l4, st, bad, deal);           \
+    return launched();                                                                                         \
+  }
+    MI_DEAL_SHAPES(X)
+#undef X
+  }
   jdesc("launch verify", (uint32_t)pl.kind * 1000u + (pl.dma ? 100u + pl.dma : pl.run_u * 10u + pl.run_nw), d, ip, l4, st,
         bad);
   if (pl.kind == kPlanRun && pl.dma) {
@@ -2421,6 +2508,9 @@ enum AqlKernelId {
 #define X(G_, U_) kAqlV_##G_##x##U_,
   MI_AQL_SHAPES(X)
 #undef X
+#define X(G_, U_) kAqlVD_##G_##x##U_,
+  MI_DEAL_SHAPES(X)
+#undef X
   kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
@@ -2431,6 +2521,9 @@ const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
     MI_AQL_SHAPES(X)
 #undef X
+#define X(G_, U_) "mi_aql_vd_" #G_ "x" #U_,
+    MI_DEAL_SHAPES(X)
+#undef X
     "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
@@ -2439,6 +2532,9 @@ const char *const kAqlNames[kAqlKernels] = {
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
+#undef X
+#define X(G_, U_) (const void *)mi_aql_vd_##G_##x##U_,
+    MI_DEAL_SHAPES(X)
 #undef X
     (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
     (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
@@ -2457,6 +2553,11 @@ struct AqlArgs {
   uint32_t *bad;
 };
 static_assert(sizeof(AqlArgs) == sizeof(BurstArgs) && sizeof(BurstArgs) <= 128, "a burst's arguments in 8 chunks");
+struct AqlDealArgs {  // mi_aql_vd_*: the verify arguments and the counter set
+  AqlArgs a;
+  uint32_t *deal;
+};
+bool aql_is_deal(int id) { return id >= kAqlVD_1x4 && id <= kAqlVD_8x12; }
 constexpr uint32_t kAqlHidden = (sizeof(AqlArgs) + 7u) & ~7u;
 
 struct AqlKernel {
@@ -2641,10 +2742,12 @@ int aql_device(int dev, AqlDevice **out) {
         (void)ldr.hsa_ven_amd_loader_iterate_executables(aql_exe_cb, &f);
       for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
         if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
-        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 40u : kAqlHidden + 66u) ||
+        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 40u
+                                   : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) + 66u : kAqlHidden + 66u) ||
                  a.k[i].kernarg > 512u)
           fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
-               i == kAqlScalar ? 56u : i == kAqlSvc ? 40u : (unsigned)sizeof(AqlArgs));
+               i == kAqlScalar ? 56u : i == kAqlSvc ? 40u
+               : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) : (unsigned)sizeof(AqlArgs));
       }
     }
   }
@@ -2668,8 +2771,21 @@ int aql_kernel_for_shape(const Desc &d, Shape sh, int *id, unsigned *blocks) {
 
 // Which mi_aql_* kernel and grid a verify pass over d gets (launch_verify's
 // plan; length-class plans need several launches per pass: not offered).
-int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks) {
+int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks, bool deal = false) {
   const Plan pl = verify_plan(d, max_len);
+  const void *dfn = nullptr;
+  if (deal && pl.kind == kPlanShape &&
+      deal_plan(d, pl.shape, [](Shape sh) -> const void * {
+#define X(G_, U_) if (sh.g == G_ && sh.u == U_) return kAqlFuncs[kAqlVD_##G_##x##U_];
+        MI_DEAL_SHAPES(X)
+#undef X
+        return nullptr;
+      }, &dfn, blocks)) {
+#define X(G_, U_) if (pl.shape.g == G_ && pl.shape.u == U_) *id = kAqlVD_##G_##x##U_;
+    MI_DEAL_SHAPES(X)
+#undef X
+    return 0;
+  }
   if (pl.kind == kPlanRun && pl.dma) {
 #define X(U_, R_)                          \
   if (pl.dma == 10 * U_ + R_) {            \
@@ -2727,8 +2843,9 @@ struct AqlRun {
   hsa_queue_t *q[4] = {};
   hsa_signal_t first{}, rest{};  // pass 0's completion (timing start) / every other pass's
   bool have_first = false, have_rest = false;
-  uint8_t *kargs = nullptr;      // device memory: one argument block per batch
+  uint8_t *kargs = nullptr;      // device memory: one argument block per (batch, queue)
   size_t kargs_bytes = 0;
+  uint32_t *deal = nullptr;      // dealt-unit counter sets, one per queue (or none)
   std::vector<hsa_kernel_dispatch_packet_t> pkt;  // one prebuilt packet per batch
   uint32_t last_steps = 0;
   bool pending = false;
@@ -2745,6 +2862,7 @@ void aql_free(AqlRun *a) {
     jnote("free aql kargs", a->kargs, a->kargs_bytes);
     (void)jfree(a->kargs);
   }
+  if (a->deal) (void)jfree(a->deal);
   delete a;
 }
 // A run whose passes never completed (a fault, a hang, a failed wait): its
@@ -2821,18 +2939,31 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
   AqlRun *a = new AqlRun();
   a->dev = dv;
   a->nq = std::min(std::max(nqueues, 1u), 4u);
+  const uint32_t nq = a->nq;
   uint32_t slot = 0;
   std::vector<int> ids(nb);
   std::vector<unsigned> blocks(nb);
+  bool any_deal = false;
   for (uint32_t j = 0; j < nb; ++j) {
-    if ((rc = aql_kernel_for(d[j], max_len[j], &ids[j], &blocks[j]))) {
+    if ((rc = aql_kernel_for(d[j], max_len[j], &ids[j], &blocks[j], true))) {
       aql_free(a);
       return rc;
     }
+    any_deal = any_deal || aql_is_deal(ids[j]);
     slot = std::max(slot, (dv->k[ids[j]].kernarg + 63u) & ~63u);
   }
-  std::vector<uint8_t> host((size_t)slot * nb, 0);
-  a->pkt.resize(nb);
+  // one argument block and packet per (batch, queue): a dealt-unit pass
+  // carries its queue's counter set (passes of one queue never overlap)
+  if (any_deal) {
+    hipError_t e = jmalloc(&a->deal, (size_t)kDealSetBytes * nq);
+    if (e == hipSuccess) e = hipMemset(a->deal, 0, (size_t)kDealSetBytes * nq);
+    if (e != hipSuccess) {
+      aql_free(a);
+      return set_err(-ENOMEM, "AQL engine: counters: %s", hipGetErrorString(e));
+    }
+  }
+  std::vector<uint8_t> host((size_t)slot * nb * nq, 0);
+  a->pkt.resize((size_t)nb * nq);
   hipError_t e = jmalloc((void **)&a->kargs, host.size());
   dbg_mem("aql-kargs", a->kargs, host.size());
   a->kargs_bytes = host.size();
@@ -2842,12 +2973,21 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
   }
   for (uint32_t j = 0; j < nb; ++j) {
-    aql_fill_args(host.data() + (size_t)slot * j,
-                  AqlArgs{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr}, blocks[j],
-                  aql_wg(ids[j]));
-    aql_fill_packet(a->pkt[j], dv->k[ids[j]], blocks[j], a->kargs + (size_t)slot * j, aql_wg(ids[j]));
+    const AqlArgs args{d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr, nullptr};
+    for (uint32_t q = 0; q < nq; ++q) {
+      const size_t k = (size_t)j * nq + q;
+      uint8_t *ka = host.data() + slot * k;
+      if (aql_is_deal(ids[j])) {
+        const AqlDealArgs da{args, a->deal + q * (kDealSetBytes / 4u)};
+        aql_fill_raw(ka, &da, sizeof da, blocks[j], aql_wg(ids[j]), ~0u);
+      } else {
+        aql_fill_args(ka, args, blocks[j], aql_wg(ids[j]));
+      }
+      aql_fill_packet(a->pkt[k], dv->k[ids[j]], blocks[j], a->kargs + slot * k, aql_wg(ids[j]));
+    }
     jdesc("  aql batch", (uint32_t)ids[j], d[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr, st ? st[j] : nullptr);
   }
+  if (a->deal) jnote("  aql deal counters", a->deal, (uint64_t)kDealSetBytes * nq);
   e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     aql_free(a);
@@ -2900,7 +3040,7 @@ int aql_wait(AqlRun *a) {
 int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
   if (!steps) return 0;
   jnote("launch aql run", a->kargs, a->kargs_bytes, steps);
-  const uint32_t nb = (uint32_t)a->pkt.size();
+  const uint32_t nb = (uint32_t)(a->pkt.size() / a->nq);
   hsa_signal_store_relaxed(a->first, 1);
   hsa_signal_store_relaxed(a->rest, (hsa_signal_value_t)(steps - 1));
   const uint16_t rel = aql_release_scope();
@@ -2932,7 +3072,7 @@ int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
     }
     hsa_kernel_dispatch_packet_t *slot =
         (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
-    const hsa_kernel_dispatch_packet_t &t = a->pkt[j];
+    const hsa_kernel_dispatch_packet_t &t = a->pkt[(size_t)j * a->nq + qi];
     // everything but the first 32 bits (header + setup), which go last
     memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
     slot->completion_signal = k == 0 ? a->first : a->rest;
@@ -3600,6 +3740,24 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
   return buf;
 }
 
+// Diagnostics (not in the public header): the verify kernel a prepared
+// submission (mi_cksum_repeat_* / mi_cksum_ipv4_verify_repeat) runs for this
+// batch -- the dealt-unit kernel when dealing applies (mi__set_deal), else
+// what mi_cksum_verify_plan names.  Needs the device (occupancy query).
+const char *mi__repeat_plan(const mi_pkt_batch *b) {
+  static thread_local char buf[96];
+  Desc d;
+  if (!b || make_desc(b, &d) || ensure_ctx()) return "invalid batch";
+  const Plan pl = verify_plan(d, batch_max_len(b));
+  const void *fn = nullptr;
+  unsigned blocks = 0;
+  if (pl.kind == kPlanShape && deal_plan(d, pl.shape, deal_kernel, &fn, &blocks)) {
+    snprintf(buf, sizeof buf, "k_ipv4_verify_dyn<%d,%d> (dealt units, %u workgroups)", pl.shape.g, pl.shape.u, blocks);
+    return buf;
+  }
+  return mi_cksum_verify_plan(b);
+}
+
 int mi_cksum_rx_offload(const mi_pkt_batch *b, uint32_t *csum_flags, uint32_t *csum_data,
                         uint32_t *bad_count, void *stream) {
   Desc d;
@@ -3647,6 +3805,11 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
     }
   }
   if (!c.rgate) HIP_TRY(hipEventCreateWithFlags(&c.rgate, hipEventDisableTiming));
+  if (!c.rdeal && deal_on()) {
+    HIP_TRY(jmalloc(&c.rdeal, (size_t)kDealSetBytes * ThreadCtx::kMaxRep));
+    HIP_TRY(hipMemset(c.rdeal, 0, (size_t)kDealSetBytes * ThreadCtx::kMaxRep));
+  }
+  auto deal_set = [&](uint32_t q) { return c.rdeal ? c.rdeal + q * (kDealSetBytes / 4u) : nullptr; };
   const bool graph = timing & MI_REPEAT_GRAPH;
   timing &= ~MI_REPEAT_GRAPH;
   if (graph && timing == MI_TIME_PER_PASS) return set_err(-EINVAL, "MI_REPEAT_GRAPH times the region only");
@@ -3685,7 +3848,7 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
       for (uint32_t k = 0; k < steps && !rc; ++k) {
         const uint32_t j = k % nb;
         rc = launch_verify(d[j], ml[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
-                           status ? status[j] : nullptr, nullptr, c.rstream[k % nstreams]);
+                           status ? status[j] : nullptr, nullptr, c.rstream[k % nstreams], deal_set(k % nstreams));
       }
       for (uint32_t q = 1; q < nstreams; ++q) {
         HIP_TRY(hipEventRecord(c.rjoin[q], c.rstream[q]));
@@ -3727,7 +3890,7 @@ int mi_cksum_ipv4_verify_repeat(const mi_pkt_batch *b, uint32_t nb, uint16_t *co
     hipStream_t st = c.rstream[k % nstreams];
     if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k], st));
     if ((rc = launch_verify(d[j], ml[j], ip ? ip[j] : nullptr, l4 ? l4[j] : nullptr,
-                            status ? status[j] : nullptr, nullptr, st)))
+                            status ? status[j] : nullptr, nullptr, st, deal_set(k % nstreams))))
       return rc;
     if (timing == MI_TIME_PER_PASS) HIP_TRY(hipEventRecord(c.ev[2 * k + 1], st));
   }
@@ -3778,6 +3941,8 @@ struct mi_repeat {
   uint32_t seq = 0;
   double trace[8] = {};  // MI_CKSUM_REPEAT_TRACE: host timestamps of the last run (s)
   AqlRun *aql = nullptr;  // MI_REPEAT_ENGINE_AQL
+  uint32_t *deal = nullptr;  // dealt-unit counter sets, one per stream (the AQL engine has its own)
+  uint32_t *deal_set(uint32_t q) const { return deal ? deal + q * (kDealSetBytes / 4u) : nullptr; }
 };
 
 namespace {
@@ -3791,6 +3956,7 @@ void repeat_free(mi_repeat *r) {
   }
   if (r->ev0) (void)hipEventDestroy(r->ev0);
   if (r->flag) (void)jhostfree(r->flag);
+  if (r->deal) (void)jfree(r->deal);
   if (r->aql) {
     if (aql_wait(r->aql) == 0) aql_free(r->aql);
     else aql_leak(r->aql);
@@ -3872,6 +4038,10 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
     if (e == hipSuccess) e = hipEventCreateWithFlags(&r->ev_done[q], hipEventDisableTiming);
   }
   if (e == hipSuccess) e = hipEventCreate(&r->ev0);
+  if (e == hipSuccess && deal_on()) {
+    e = jmalloc(&r->deal, (size_t)kDealSetBytes * nstreams);
+    if (e == hipSuccess) e = hipMemset(r->deal, 0, (size_t)kDealSetBytes * nstreams);
+  }
   if (e == hipSuccess && repeat_wait_mode() == kWaitFlag) {
     e = jhostmalloc((void **)&r->flag, 64 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&r->flag_dev, r->flag, 0);
@@ -3932,7 +4102,7 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
     if (r->op == MI_REPEAT_OP_FINALIZE)
       rc = launch_finalize(r->d[j], pick_shape(r->ml[j]), r->s[k % ns], r->mlen[j]);
     else
-      rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns]);
+      rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns], r->deal_set(k % ns));
     t_lev = LaunchEv();
     if (rc) return rc;
     j = j + 1 == r->nb ? 0 : j + 1;
@@ -4939,6 +5109,13 @@ int mi__set_dropin_service(int on) {
 }
 // Is the calling thread's drop-in service running?  (tests)
 int mi__dropin_service_live(void) { return t_aql1.svc_live ? 1 : 0; }
+// Tests / A-B runs: dealt units for the prepared submissions on (1) or off
+// (0); returns the previous setting.  Takes effect for handles created after.
+int mi__set_deal(int on) {
+  const int was = deal_on() ? 1 : 0;
+  g_deal.store(on ? 1 : 0);
+  return was;
+}
 // Tests: the calling thread's last drop-in tag (the next call uses the one
 // after it), and the number of threads holding a service slot.
 void mi__set_dropin_tag(uint32_t tag) { t_ctx.stag = tag & 0xffffu; }

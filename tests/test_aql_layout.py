@@ -53,13 +53,16 @@ def test_aql_entry_points_kernarg_layout(tmp_path):
     ks = _kernels(tmp_path)
     verify = [k for k in ks if k not in ("mi_aql_scalar", "mi_aql_dropin_svc")]
     assert "mi_aql_v_16x6" in ks and "mi_aql_run8" in ks and "mi_aql_slot64" in ks and "mi_aql_scalar" in ks
+    assert "mi_aql_vd_16x6" in ks and "mi_aql_vd_8x12" in ks
     for name in verify:
         args, seg = ks[name]
         explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]
-        assert explicit == [(0, 80), (80, 8), (88, 8), (96, 8), (104, 8)], (name, explicit)
+        # mi_aql_vd_*: one more argument, the queue's dealt-unit counter set (AqlDealArgs)
+        deal = name.startswith("mi_aql_vd_")
+        assert explicit == [(0, 80), (80, 8), (88, 8), (96, 8), (104, 8)] + ([(112, 8)] if deal else []), (name, explicit)
         for o, s, k in args:
             if k in HIDDEN:
-                assert o == VERIFY_EXPLICIT + HIDDEN[k], (name, k, o)
+                assert o == VERIFY_EXPLICIT + (8 if deal else 0) + HIDDEN[k], (name, k, o)
         assert seg <= 512, (name, seg)
     args, seg = ks["mi_aql_scalar"]
     explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]

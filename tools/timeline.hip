@@ -135,6 +135,23 @@ __global__ __launch_bounds__(kBlock, 5) void tl_multi(MultiArgs a, uint32_t *tl,
   put_rec(tl, tl_bytes, w0 + blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6), t0, t1, t2, units * gpw);
 }
 
+// verify_dyn_body (dealt units, round 5) with stamps: the first stamp after
+// the wave's first unit, the unit count in the record
+template <int G, int U>
+__global__ __launch_bounds__(kBlock) void tl_dyn(Desc d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
+                                                 uint32_t *deal, uint32_t *tl, uint32_t tl_bytes, uint32_t w0) {
+  const uint64_t t0 = stamp();
+  uint64_t t1 = 0;
+  uint32_t units = 0;
+  verify_dyn_body<G, U>(d, ip_out, l4_out, st_out, nullptr, deal, [&]() {
+    if (!units) t1 = stamp();
+    ++units;
+  });
+  if (!units) t1 = stamp();
+  const uint64_t t2 = stamp();
+  put_rec(tl, tl_bytes, w0 + blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6), t0, t1, t2, units * (64u / G));
+}
+
 Desc desc_of(const mi_pkt_batch &b) {
   Desc d{};
   d.base = (const uint8_t *)b.base;
@@ -174,12 +191,22 @@ float tl_run(int mode, const mi_pkt_batch *b, int nb, uint16_t *const *ip, uint1
   }
   if (hipEventCreate(&e0) != hipSuccess) return -3.f;
   const uint32_t waves = (uint32_t)grid * (kBlock / 64);
+  uint32_t *deal = nullptr;  // mode 2: one counter set per stream, zeroed (each launch leaves it zeroed)
+  if (mode == 2) {
+    if (hipMalloc(&deal, (size_t)kDealSetBytes * nstreams) != hipSuccess) return -3.f;
+    (void)hipMemset(deal, 0, (size_t)kDealSetBytes * nstreams);
+    (void)hipDeviceSynchronize();
+  }
   (void)hipEventRecord(e0, s[0]);
   for (int q = 1; q < nstreams; ++q) hipStreamWaitEvent(s[q], e0, 0);
   for (int k = 0; k < launches; ++k) {
     hipStream_t q = s[k % nstreams];
     const uint32_t w0 = (uint32_t)k * waves;
-    if (mode == 0) {
+    if (mode == 2) {
+      const int j = k % nb;
+      hipLaunchKernelGGL((tl_dyn<16, 6>), dim3(grid), dim3(kBlock), 0, q, desc_of(b[j]), ip[j], l4[j], st[j],
+                         deal + (k % nstreams) * (kDealSetBytes / 4u), tl, tl_bytes, w0);
+    } else if (mode == 0) {
       const int j = k % nb;
       const Desc d = desc_of(b[j]);
       if (shape_g == 16 && shape_u == 6)
@@ -222,13 +249,16 @@ float tl_run(int mode, const mi_pkt_batch *b, int nb, uint16_t *const *ip, uint1
     hipStreamDestroy(s[q]);
   }
   hipEventDestroy(e0);
+  if (deal) (void)hipFree(deal);
   return span * 1000.f;
 }
 
 // Occupancy of the instrumented kernels (blocks per CU), for the grid choice.
 int tl_occupancy(int mode) {
   int per_cu = 0;
-  if (mode == 0)
+  if (mode == 2)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)tl_dyn<16, 6>, kBlock, 0);
+  else if (mode == 0)
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)tl_verify<16, 6>, kBlock, 0);
   else
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)tl_multi<8, 2>, kBlock, 0);

@@ -89,6 +89,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--launches", type=int, default=24)
     ap.add_argument("--rotate", type=int, default=24)
+    ap.add_argument("--only", default="", help="comma-separated name prefixes of the shapes to run")
     a = ap.parse_args()
     lib = C.CDLL(os.path.join(ROOT, "tools", "libtimeline.so"))
     lib.tl_run.restype = C.c_float
@@ -114,7 +115,7 @@ def main():
     arr = (PktBatchC * R)(*[b.c for b in bs])
     VP = C.c_void_p * R
     ips, l4s, sts = (VP(*[o[k].data_ptr() for o in outs]) for k in ("ip", "l4", "status"))
-    occ = {m: lib.tl_occupancy(m) for m in (0, 1)}
+    occ = {m: lib.tl_occupancy(m) for m in (0, 1, 2)}
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     print(json.dumps(dict(occupancy_blocks_per_cu=occ, cus=cus)), flush=True)
     K = a.launches
@@ -124,7 +125,13 @@ def main():
         ("single_16x6_isolated", 0, 1, 1, 2048),     # one launch, synchronize, next
         ("multi_8x2_x16_1stream", 1, 16, 1, occ[1] * cus),
         ("multi_8x2_x4_1stream", 1, 4, 1, occ[1] * cus),
+        # round 5: dealt units (verify_dyn_body), one resident generation
+        ("dealt_16x6_1stream", 2, 1, 1, occ[2] * cus),
+        ("dealt_16x6_2streams", 2, 1, 2, occ[2] * cus),
+        ("dealt_16x6_isolated", 2, 1, 1, occ[2] * cus),
     ]
+    if a.only:
+        shapes = [s for s in shapes if any(s[0].startswith(p) for p in a.only.split(","))]
     for name, mode, per, nst, grid in shapes:
         waves = grid * 4
         tl = torch.zeros(K * waves * 8, dtype=torch.int32, device=dev)
