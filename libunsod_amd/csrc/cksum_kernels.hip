@@ -1595,7 +1595,11 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
       uint32_t served = 0;
       if (sq != last) {
         t_seen = rt_clock();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        // (no acquire fence here: the fields and inline bytes below are
+        // system-scope loads of the mailbox, issued after the sequence word
+        // was seen, and a system-scope acquire invalidates the XCD's L2 --
+        // per request, under the batch kernels sharing it; the staged and
+        // burst paths below take the one they need)
         const uint32_t nck = (sq >> 16) & 0xffu;
         uint32_t f = 0;
         u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
