@@ -1514,29 +1514,41 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
   if (threadIdx.x == 0) scalar_result(out, tag, res, (tag >> 31) != 0u, t0);
 }
 
-// The drop-in service (MI_CKSUM_DROPIN_SERVICE): one workgroup that stays
-// resident while its thread keeps calling drop-ins, so a call costs no queue
-// dispatch.  The host writes the request into a mailbox -- fine-grained
-// device memory written through the PCIe BAR when the platform maps it for the
-// CPU, else coherent page-locked host memory: box[2..10] = off, len,
-// abs_lanes, pseudo, src, dst, proto, plen, trace; a span of at most
-// kSvcInlineBytes staging bytes (offset included) at box[kSvcInline..], else
-// the span stays in the page-locked staging buffer; then box[0], the request's
-// sequence word, last: the call's 16-bit tag, the inline span's 16-byte chunk
-// count in bits 16..23, bit 31 for a stop request.  Lane 0 polls box[0]; once
-// it moves, ONE round trip brings the fields (lanes 2..10) and the inline
-// chunks (two per lane at most), and an inline span is folded by wave 0 alone;
-// a staged one by the whole workgroup (scalar_span).  The result goes to the
-// caller's pinned word as mi_aql_scalar stores it.  Exit conditions every wave
-// reaches: a stop request, or no new request for idle_ticks of the 100 MHz
-// clock -- the host sees the
-// dispatch retire (its completion signal) and launches a new one when the next
-// call comes.  With trace set, out[2..5] get the clock at the moment the
-// request was seen and at the result store.  On its way out the service
-// stores its launch token at out[6]: the process-exit handler waits for that
-// word (svc_atexit), so no service is still running when the runtime tears
-// the process's memory down.
+// The drop-in service (MI_CKSUM_DROPIN_SERVICE, round 5: ONE per device, for
+// every calling thread).  A resident workgroup on the device's drop-in queue
+// serves the (b1) drop-ins and small host RX bursts of all threads from a slab
+// of mailbox SLOTS -- fine-grained device memory the host writes through the
+// PCIe BAR when the platform maps it for the CPU, else coherent page-locked
+// host memory -- so a call costs no queue dispatch, and however many threads
+// call, the batch path shares the command processor with one more queue, not
+// one per thread (per-thread queues cut the 1500 B batch rate to
+// 0.27-0.65x with 2-16 calling threads, profiles/r05/service_interference_*).
+//
+// Slot k (kSvcSlotWords words; slot kSvcSlots's first word is the control
+// word): [kBoxSeq] the request's sequence word, written last -- the call's
+// 16-bit tag, the inline span's 16-byte chunk count in bits 16..23, bit 30 for
+// a burst; [kBoxAck] the sequence word the service last served (written before
+// the result; read by the next launch); [2..10] off, len, abs_lanes, pseudo, src, dst, proto, plen,
+// trace; [kBoxStageBytes], [kBoxStage] the thread's page-locked staging buffer
+// (bytes, device address) and [kBoxOut] its result block; [kSvcInline..] a
+// span of at most kSvcInlineBytes staging bytes (offset included), or a
+// burst's arguments and descriptors.  Wave 0 polls every slot's sequence word
+// and the control word with ONE load per lane; a slot whose word moved is
+// served (fields and inline chunks with one round trip; an inline span by wave
+// 0 alone, a staged span or a burst by the whole workgroup), acknowledged, and
+// its result stored into the thread's result block as mi_aql_scalar stores it.
+// Exit conditions every wave reaches: the control word moves (process exit),
+// or no slot moved for idle_ticks of the 100 MHz clock -- the next caller sees
+// the dispatch retire (its completion signal) and launches a new one, which
+// starts from the slots' acknowledged words, so a request posted as the old
+// one left is served by the new one.  On its way out the service stores its
+// launch token at *exitw: the process-exit handler waits for that word
+// (svc_atexit).  With trace set, out[2..5] get the clock at the moment the
+// request was seen and at the result store.
 constexpr uint32_t kSvcInline = 16, kSvcInlineBytes = 2048, kSvcWords = kSvcInline + kSvcInlineBytes / 4;
+constexpr uint32_t kSvcSlots = 63, kSvcSlotWords = 1024;  // slots per device (+ the control word's), 4 KiB each
+enum : uint32_t { kBoxSeq = 0, kBoxAck = 1, kBoxStageBytes = 11, kBoxOut = 12, kBoxStage = 14 };
+static_assert(kSvcWords <= kSvcSlotWords && kSvcSlots < 64, "a slot per lane of the polling wave, the control word last");
 // A host-memory RX burst for the service (bit 30 of the sequence word): the
 // verify kernels' arguments (AqlArgs' layout), carried in the mailbox's inline
 // area; the descriptors follow them there.
@@ -1570,92 +1582,120 @@ __device__ __forceinline__ void svc_burst(const BurstArgs &a) {
                   a.l4, a.st, a.bad, d);
   }
 }
-extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint8_t *base, uint32_t bytes,
-                                                                             uint32_t token, const uint32_t *box,
-                                                                             uint32_t *out, uint32_t seq0,
+extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint32_t *slab, uint32_t nslots,
+                                                                             uint32_t *exitw, uint32_t token,
                                                                              uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
-  __shared__ uint32_t req[13];  // [0] sequence, [2..10] fields, [11] a burst, [12] served by wave 0
-  __shared__ u32x4 s_args[8];   // a burst's BurstArgs
-  const Arr mb = arr_of(box, 4u * kSvcWords);  // the mailbox, read at system scope
-  uint32_t last = seq0;
+  __shared__ uint32_t req[16];  // [0] sequence, [1] slot, [2..10] fields, [11] a burst, [12] served by wave 0,
+                                // [13] exit, [14..15] the staging buffer's bytes / low half of its address
+  __shared__ uint64_t s_ptr[2];  // the slot's result block and staging buffer
+  __shared__ u32x4 s_args[8];    // a burst's BurstArgs
+  const Arr mb = arr_of(slab, 4ull * kSvcSlotWords * (kSvcSlots + 1));  // the slab, read at system scope
+  // nslots: the slots in bits 0..7, the poll period in bits 8..15 (in units
+  // of s_sleep 1, 64 clocks; 0 = 1)
+  const uint32_t ns = (nslots & 0xffu) < kSvcSlots ? (nslots & 0xffu) : kSvcSlots;
+  const uint32_t poll = (nslots >> 8) & 0xffu;
+  // wave 0, lane k < ns: slot k's last served sequence word (its ack word at
+  // launch); lane 63: the control word at launch
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t my_word = lane < ns ? lane * kSvcSlotWords + kBoxSeq : lane == 63u ? kSvcSlots * kSvcSlotWords : kOOB;
+  uint32_t last = 0;
+  if (threadIdx.x < 64)
+    last = lane < ns ? ld_u32<kSys | kVolatile>(mb, lane * kSvcSlotWords + kBoxAck)
+                     : ld_u32<kSys | kVolatile>(mb, my_word);
   uint64_t t_last = rt_clock(), t_seen = 0;
   for (;;) {
     if (threadIdx.x < 64) {
-      const uint32_t lane = threadIdx.x;
-      uint32_t sq = last;
-      if (lane == 0) {
-        for (;;) {
-          sq = ld_u32<kSys | kVolatile>(mb, 0u);
-          if (sq != last || rt_clock() - t_last > idle_ticks) break;
-          __builtin_amdgcn_s_sleep(1);
+      uint32_t w = 0, s = ~0u;
+      bool stop = false;
+      for (;;) {
+        w = ld_u32<kSys | kVolatile>(mb, my_word);
+        const uint64_t pend = __ballot(lane < ns && w != last);
+        stop = __builtin_amdgcn_readlane((int)(w ^ last), 63) != 0;
+        if (pend) {
+          s = (uint32_t)__builtin_ctzll(pend);
+          break;
         }
+        if (stop || rt_clock() - t_last > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+        for (uint32_t k = 1; k < poll; ++k) __builtin_amdgcn_s_sleep(1);
       }
-      sq = __builtin_amdgcn_readfirstlane(sq);
-      uint32_t served = 0;
-      if (sq != last) {
+      uint32_t served = 0, burst = 0, sq = 0;
+      if (s != ~0u) {
         t_seen = rt_clock();
-        // (no acquire fence here: the fields and inline bytes below are
-        // system-scope loads of the mailbox, issued after the sequence word
-        // was seen, and a system-scope acquire invalidates the XCD's L2 --
-        // per request, under the batch kernels sharing it; the staged and
-        // burst paths below take the one they need)
+        sq = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)s);
+        if (lane == s) last = sq;  // (served below, before the next poll)
+        // (no acquire fence: the fields and inline bytes are system-scope
+        // loads of the slot, issued after its sequence word was seen, and a
+        // system-scope acquire invalidates the XCD's L2 -- per request, under
+        // the batch kernels sharing it)
+        const uint32_t base = s * kSvcSlotWords;
         const uint32_t nck = (sq >> 16) & 0xffu;
-        uint32_t f = 0;
         u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
         auto ld4 = [&](uint32_t c) {
-          const uint32_t q = kSvcInline + 4u * c;
+          const uint32_t q = base + kSvcInline + 4u * c;
           return u32x4{ld_u32<kSys | kVolatile>(mb, q), ld_u32<kSys | kVolatile>(mb, q + 1u),
                        ld_u32<kSys | kVolatile>(mb, q + 2u), ld_u32<kSys | kVolatile>(mb, q + 3u)};
         };
-        if (lane >= 2 && lane < 11) f = ld_u32<kSys | kVolatile>(mb, lane);
-        if (!(sq >> 31)) {
-          if (lane < nck) v0 = ld4(lane);
-          if (64u + lane < nck) v1 = ld4(64u + lane);
-        }
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane(f, 2), len = (uint32_t)__builtin_amdgcn_readlane(f, 3);
-        const bool burst = !(sq >> 31) && ((sq >> 30) & 1u);
+        const uint32_t f = lane < 16u ? ld_u32<kSys | kVolatile>(mb, base + lane) : 0u;
+        if (lane < nck) v0 = ld4(lane);
+        if (64u + lane < nck) v1 = ld4(64u + lane);
+        auto field = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k); };
+        const uint64_t out = (uint64_t)field(kBoxOut) | ((uint64_t)field(kBoxOut + 1) << 32);
+        burst = (sq >> 30) & 1u;
         if (burst && lane < nck && lane < 8u) s_args[lane] = v0;
-        if (lane == 0) req[11] = burst ? 1u : 0u;
-        if (!(sq >> 31) && !burst && nck) {
+        if (!burst && nck) {
           // the inline span: its staging bytes [0, off + len) sit at the inline
           // area's start (64-byte aligned, so address parity is the staging's)
+          const uint32_t off = field(2), len = field(3);
           uint32_t acc = range_sum(v0, (int)(16u * lane) - (int)off, 0, (int)len) +
                          range_sum(v1, (int)(16u * (64u + lane)) - (int)off, 0, (int)len);
           acc = group_sum<64>(acc);
           if (lane == 0) {
-            const uint32_t abs_lanes = (uint32_t)__builtin_amdgcn_readlane(f, 4),
-                           pseudo = (uint32_t)__builtin_amdgcn_readlane(f, 5);
             uint64_t sum = fold16_64(acc);
-            if (!abs_lanes && (off & 1u)) sum = swap16((uint32_t)sum);
+            if (!field(4) && (off & 1u)) sum = swap16((uint32_t)sum);
             // (readlane returns int: through uint32_t, or a source address
             // above 2^31 would be sign-extended into the 64-bit sum)
-            const uint32_t src = (uint32_t)__builtin_amdgcn_readlane(f, 6), dst = (uint32_t)__builtin_amdgcn_readlane(f, 7),
-                           proto = (uint32_t)__builtin_amdgcn_readlane(f, 8),
-                           plen = (uint32_t)__builtin_amdgcn_readlane(f, 9);
-            if (pseudo) sum += (uint64_t)src + dst + (proto << 8) + swap16(plen & 0xffffu);
+            if (field(5)) sum += (uint64_t)field(6) + field(7) + (field(8) << 8) + swap16(field(9) & 0xffffu);
             const uint32_t res = ~fold16_64(sum) & 0xffffu;
-            scalar_result(out, sq, res, __builtin_amdgcn_readlane(f, 10) != 0u, t_seen);
+            st_u32<kSys>(mb, base + kBoxAck, sq);  // (read by the next launch, after this one retired)
+            scalar_result((uint32_t *)out, sq, res, field(10) != 0u, t_seen);
           }
           served = 1;
         }
         if (lane >= 2 && lane < 11) req[lane] = f;
+        if (lane == 0) {
+          s_ptr[0] = out;
+          s_ptr[1] = (uint64_t)field(kBoxStage) | ((uint64_t)field(kBoxStage + 1) << 32);
+          req[14] = field(kBoxStageBytes);
+        }
       }
       if (lane == 0) {
         req[0] = sq;
+        req[1] = s;
+        req[11] = burst;
         req[12] = served;
+        req[13] = s == ~0u ? 1u : 0u;  // idle or a stop: leave
       }
     }
     __syncthreads();
-    const uint32_t sq = req[0];
-    if (sq == last || (sq >> 31)) {  // idle, or a stop request
-      if (threadIdx.x == 0) st_u32<kSys>(arr_of(out, 4u * kOutWords), 6u, token);
+    if (req[13]) {
+      if (threadIdx.x == 0) st_u32<kSys>(arr_of(exitw, 4u), 0u, token);
       break;
     }
+    const uint32_t sq = req[0], s = req[1];
+    uint32_t *const out = (uint32_t *)s_ptr[0];
     if (req[11]) {
       // a host RX burst: every wave, then the result word once every wave's
-      // outputs are visible at system scope
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      // outputs are visible at system scope.  field 2: diagnostics only
+      // (MI_CKSUM_BURST_FENCES, tools/burst_breakdown.py): bit 0 drops the
+      // acquire, bit 1 replaces the release by a wait for the stores' acks;
+      // field 10 (trace): out[1], out[6], out[7] get the clock after the
+      // acquire, after the burst and after the release, from the request seen
+      const uint32_t mode = req[2];
+      const bool trace = req[10] != 0u;
+      if (!(mode & 1u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      const uint64_t ta = rt_clock();
       // the arguments, wave-uniform (they build the burst's resources)
       uint32_t w[sizeof(BurstArgs) / 4];
 #pragma unroll
@@ -1664,20 +1704,51 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
       BurstArgs a;
       __builtin_memcpy(&a, w, sizeof a);
       svc_burst(a);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      uint64_t tb = 0;
+      if (trace) {
+        __syncthreads();
+        tb = rt_clock();
+      }
+      if (!(mode & 2u))
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      else
+        __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      if (threadIdx.x == 0) scalar_result(out, sq, 0u, false, t_seen);
+      if (threadIdx.x == 0) {
+        st_u32<kSys>(mb, s * kSvcSlotWords + kBoxAck, sq);
+        if (trace) {
+          const Arr ob = arr_of(out, 4u * kOutWords);
+          const uint64_t tc = rt_clock();
+          st_u32<kSys>(ob, 1u, (uint32_t)(ta - t_seen));
+          st_u32<kSys>(ob, 6u, (uint32_t)(tb - t_seen));
+          st_u32<kSys>(ob, 7u, (uint32_t)(tc - t_seen));
+        }
+        scalar_result(out, sq, 0u, trace, t_seen);
+      }
     } else if (!req[12]) {
-      // every wave: the staging bytes are ordinary page-locked memory the host
-      // rewrote since the last request -- no cached copy of them may be used
+      // a staged span, every wave: the staging bytes are ordinary page-locked
+      // memory the host rewrote since its last request -- no cached copy of
+      // them may be used
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-      const uint32_t res = scalar_span(base, bytes, req[2], req[3], req[4], req[5], req[6], req[7], req[8], req[9], part);
-      if (threadIdx.x == 0) scalar_result(out, sq, res, req[10] != 0u, t_seen);
+      const uint8_t *stage = (const uint8_t *)(((uint64_t)__builtin_amdgcn_readfirstlane((int)(s_ptr[1] >> 32)) << 32) |
+                                               (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_ptr[1]));
+      const uint32_t res = scalar_span(stage, req[14], req[2], req[3], req[4], req[5], req[6], req[7], req[8], req[9], part);
+      if (threadIdx.x == 0) {
+        st_u32<kSys>(mb, s * kSvcSlotWords + kBoxAck, sq);
+        scalar_result(out, sq, res, req[10] != 0u, t_seen);
+      }
     }
-    last = sq;
     t_last = rt_clock();
     __syncthreads();  // req[] and part[] are rewritten by the next request
   }
+}
+
+// Diagnostics (tools/service_idle_probe.py): one wave that stays resident for
+// `ticks` of the 100 MHz clock and touches no memory -- what any resident
+// kernel, apart from the service's polling, costs the batch path.
+extern "C" __global__ __launch_bounds__(64) void mi_aql_spin(uint64_t ticks) {
+  const uint64_t t0 = rt_clock();
+  while (rt_clock() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
 namespace {
@@ -2519,7 +2590,7 @@ enum AqlKernelId {
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
-  kAqlSlot64, kAqlScalar, kAqlSvc, kAqlKernels
+  kAqlSlot64, kAqlScalar, kAqlSvc, kAqlSpin, kAqlKernels
 };
 const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
@@ -2532,7 +2603,7 @@ const char *const kAqlNames[kAqlKernels] = {
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    "mi_aql_slot64", "mi_aql_scalar", "mi_aql_dropin_svc"};
+    "mi_aql_slot64", "mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin"};
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
@@ -2545,7 +2616,7 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar, (const void *)mi_aql_dropin_svc};
+    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar, (const void *)mi_aql_dropin_svc, (const void *)mi_aql_spin};
 
 // The kernels' explicit arguments, laid out as the compiler lays out the
 // kernel-argument segment (each parameter at its natural alignment).  The
@@ -2575,14 +2646,29 @@ struct AqlDevice {
   hsa_agent_t agent{};
   double ns_per_tick = 1.0;
   AqlKernel k[kAqlKernels];
-  // the drop-in service's mailboxes: fine-grained device memory the host
-  // writes through the PCIe BAR (mbox_tried / mbox_ok: found once), carved
-  // from one slab of kMboxSlots 4 KiB slots that is never freed
-  bool mbox_tried = false, mbox_ok = false;
+  // the drop-in queue and service (dq_open, svc_ensure): one HSA queue for
+  // every thread's drop-in and host-burst dispatches and the resident service
+  // on it; the mailbox slab (slab_alloc: BAR-mapped VRAM when the platform
+  // allows it, mbox_*), its slot bitmap and each slot's last posted sequence
+  // word (written only by the slot's owner)
+  std::mutex dq_mu;
+  int dq_rc = 0;
+  hsa_queue_t *dq = nullptr, *sq = nullptr;  // dispatches; the service (a packet behind a running
+                                             // kernel on one queue waits for it, barrier bit or not)
+  std::atomic<int> dq_err{0};
+  hsa_signal_t svc_sig{};  // 1 while a service dispatch runs
+  std::atomic<bool> svc_launched{false};
+  uint32_t svc_token = 0;  // the latest launch's token
+  uint8_t *svc_karg = nullptr;
+  volatile uint32_t *svc_host = nullptr;  // coherent page-locked: [0] the exiting service's token
+  uint32_t *svc_host_dev = nullptr;
+  uint32_t ctl = 0;  // the control word's value
+  bool mbox_ok = false, slab_vram = false;
   hsa_amd_memory_pool_t mbox_pool{};
   hsa_agent_t cpu{};
-  uint8_t *mbox_slab = nullptr;
-  uint64_t mbox_used = 0;  // slot bitmap
+  uint32_t *slab = nullptr, *slab_dev = nullptr;
+  uint64_t slot_used = 0;
+  uint32_t slot_seq[64] = {};
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -2746,11 +2832,11 @@ int aql_device(int dev, AqlDevice **out) {
         (void)ldr.hsa_ven_amd_loader_iterate_executables(aql_exe_cb, &f);
       for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
         if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
-        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 40u
+        else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 32u : i == kAqlSpin ? 8u
                                    : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) + 66u : kAqlHidden + 66u) ||
                  a.k[i].kernarg > 512u)
           fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
-               i == kAqlScalar ? 56u : i == kAqlSvc ? 40u
+               i == kAqlScalar ? 56u : i == kAqlSvc ? 32u : i == kAqlSpin ? 8u
                : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) : (unsigned)sizeof(AqlArgs));
       }
     }
@@ -3118,63 +3204,57 @@ int aql_span(AqlRun *a, float *span_us) {
   return 0;
 }
 
-// One synchronous dispatch per call (the host-memory burst path): a per-thread
-// HSA queue, kernel arguments written into page-locked host memory per call
-// (the burst's descriptors change every time), acquire and release at system
-// scope (the burst and the outputs live in host memory), a spin on the
-// completion signal.  Replaces a HIP launch + hipStreamSynchronize.
+// ------------------------------------ the drop-in queue and the drop-in service
 //
-// Lifetime rule: nothing a dispatch references (its kernel-argument slot, the
-// scalar staging buffer, the queue) is rewritten, freed or destroyed before
-// the dispatch is done with it.
-//  * wait = true (host bursts): the packet carries the completion signal and
-//    the call spins on it -- retired on return.
-//  * wait = false (the (b1) drop-ins): no completion signal (a signal costs
-//    its completion event on every call, ~1.5 us, profiles/r03); the caller
-//    spins on the result word the kernel stores as its last action, after
-//    every read of its arguments and of the staging buffer -- so the next call
-//    may rewrite both, and a slot is reused only kAqlOneSlots calls later.
-//    Before the staging buffer is freed or the queue destroyed,
-//    aql_one_quiesce appends a barrier-AND packet with the signal: it
-//    completes once every earlier packet has retired.
+// The (b1) drop-ins and the host RX bursts are synchronous calls from any
+// number of application threads.  Round 4 gave every calling thread its own
+// HSA queue and, in service mode, its own resident service.  Beside the batch
+// path that cost the batch path half its rate and more: with 2-16 threads
+// calling drop-ins, the 1500 B batch rate fell to 0.27-0.65x, while idle extra
+// queues cost nothing -- queues that hold work compete for the command
+// processor (tools/queue_probe.py, tools/service_interference.py,
+// profiles/r05/queue_probe_r05.jsonl, service_interference_*).  So a device
+// has ONE queue for all their dispatches (dq: producers serialize on dq_mu)
+// and ONE service (mi_aql_dropin_svc, on a queue of its own, sq: a packet
+// behind a running kernel on the same queue waits for it to end, barrier bit
+// or not -- measured, tools/svc_probe.py: a 200-datagram burst dispatched
+// behind the service took its 1 ms idle exit) that serves every thread's
+// mailbox slot.  A thread keeps its own kernel-argument blocks and completion
+// signal; its slot is taken with its first service call and given back at
+// thread exit.
+//
+// Lifetime rule: nothing a dispatch references is rewritten or freed before
+// the dispatch is done with it.  Every call is synchronous: a waited dispatch
+// (bursts) has retired when the call returns; an unwaited one (a drop-in in
+// dispatch mode: no completion signal, ~1.5 us of completion processing saved
+// per call, profiles/r03) and the service store the result word as their last
+// access to the call's arguments, staging buffer and slot.  A wait that fails
+// (a fault, the 10 s deadline) marks the thread stuck: its argument blocks,
+// signal, slot and buffers are then leaked, never freed under a kernel that
+// may still run.  The queue, the service's argument block and the slab live as
+// long as the process.
 struct AqlOne {
   int device = -1;
   AqlDevice *dev = nullptr;
-  hsa_queue_t *q = nullptr;
   hsa_signal_t sig{};
   uint8_t *karg = nullptr;  // page-locked, mapped: kAqlOneSlots blocks of 512 B
   uint32_t next = 0;
-  bool unretired = false;   // unsignalled dispatches whose retirement nobody has seen
-  // the queue's error slot (aql_queue_error's callback data): on the heap, not
-  // in thread-local storage, so a queue leaked after a failed quiesce can still
-  // report into it after the thread has gone (it is leaked with the queue)
-  std::atomic<int> *err = nullptr;
-  int error() const { return err ? err->load() : 0; }
-  // the drop-in service (mi_aql_dropin_svc) running on this queue, and its
-  // mailbox: fine-grained device memory the host writes through the BAR
-  // (mbox_dev), else coherent page-locked host memory (ThreadCtx::sout + 16
-  // words).  The host never reads it back: mbox_seq shadows its sequence word.
-  bool svc_live = false;
-  uint32_t *mbox = nullptr;
-  bool mbox_dev = false;
-  uint32_t mbox_seq = 0;
-  bool svc_owner = false;              // holds one of the process's service slots (svc_allowed)
-  uint32_t svc_token = 0;              // the running service's launch token
-  volatile uint32_t *svc_out = nullptr;  // its result block (host): [6] = token on exit
-  bool svc_registered = false;         // in g_svc_reg (the process-exit handler's list)
+  bool stuck = false;       // a dispatch or request of this thread never finished
+  int slot = -1;            // its mailbox slot on dev (-1: none)
+  uint64_t hdr_out = 0, hdr_stage = 0;  // what the slot's header holds
+  uint32_t hdr_bytes = 0;
 };
 constexpr uint32_t kAqlOneSlots = 8;
 thread_local AqlOne t_aql1;
 
 // Drop-in latency breakdown (diagnostics, mi__dropin_trace): with tracing on,
-// the thread's drop-in dispatches carry the completion signal and queue
-// profiling, and each call records, in the HSA system timestamp domain: fold
-// entry, the doorbell written, the kernel's start and end (dispatch
-// timestamps converted to the system domain), the result word seen by the
-// host.
+// each call records, in the HSA system timestamp domain, fold entry, the
+// doorbell written (or the request posted) and the result word seen by the
+// host; the kernel stores its own start and end on the GPU's clock.
 struct DropinTrace {
   bool on = false;
   uint64_t t_entry = 0, t_doorbell = 0, t_seen = 0, g_start = 0, g_end = 0;
+  uint32_t b_acq = 0, b_body = 0, b_rel = 0;  // a service burst: GPU ticks from the request seen
   double us_per_tick = 0.0;
 };
 thread_local DropinTrace t_dtrace;
@@ -3184,205 +3264,15 @@ uint64_t sys_ts() {
   return t;
 }
 
-// Reserve the next packet slot of the thread's queue (deadline-bounded).
-int aql_one_slot(AqlOne &o, uint64_t *idx, void **slot) {
-  *idx = hsa_queue_add_write_index_screlease(o.q, 1);
-  const double t0 = mono_s();
-  while (*idx - hsa_queue_load_read_index_scacquire(o.q) >= o.q->size) {
-    if (o.error()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.error());
-    if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: queue full for 10 s");
-  }
-  *slot = (hsa_kernel_dispatch_packet_t *)o.q->base_address + (*idx & (o.q->size - 1));
-  return 0;
-}
-// Spin (deadline-bounded) until the signal reads 0.
-int aql_one_wait(AqlOne &o) {
-  const double t0 = mono_s();
-  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
-    if (o.error()) return set_err(-EIO, "AQL engine: queue error 0x%x", o.error());
-    if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
-  }
-  return 0;
-}
-// Stop the thread's drop-in service and wait for its dispatch to retire: a
-// stop request (cmd 1) under a sequence word no tag can equal (bit 16 set).
-// Post a request: fields (and inline bytes) first, the sequence word last; a
-// device mailbox is write-combined BAR memory, hence the store fences.
-void mbox_post(AqlOne &o, uint32_t seq) {
-  if (o.mbox_dev) _mm_sfence();
-  __atomic_store_n(&o.mbox[0], seq, __ATOMIC_RELEASE);
-  if (o.mbox_dev) _mm_sfence();
-  o.mbox_seq = seq;
-}
-int svc_stop(AqlOne &o) {
-  if (!o.svc_live) return 0;
-  mbox_post(o, 0x80000000u | ((o.mbox_seq + 1u) & 0xffffu));  // bit 31: stop
-  int rc = aql_one_wait(o);
-  if (rc) return rc;
-  o.svc_live = false;
-  o.unretired = false;  // its barrier bit ordered it after every earlier packet
-  return 0;
-}
-
-// Every packet of the thread's queue retired (a barrier-AND packet behind them).
-int aql_one_quiesce(AqlOne &o) {
-  int src = svc_stop(o);
-  if (src) return src;
-  if (!o.unretired) return 0;
-  uint64_t idx;
-  void *p;
-  int rc = aql_one_slot(o, &idx, &p);
-  if (rc) return rc;
-  hsa_barrier_and_packet_t *bp = (hsa_barrier_and_packet_t *)p;
-  memset((uint8_t *)bp + 4, 0, sizeof *bp - 4);
-  bp->completion_signal = o.sig;
-  hsa_signal_store_relaxed(o.sig, 1);
-  const uint32_t sc = HSA_FENCE_SCOPE_SYSTEM;
-  const uint32_t hs = (HSA_PACKET_TYPE_BARRIER_AND << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
-                      (sc << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (sc << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
-  __atomic_store_n((uint32_t *)bp, hs, __ATOMIC_RELEASE);
-  hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
-  if ((rc = aql_one_wait(o))) return rc;
-  o.unretired = false;
-  return 0;
-}
-
-// Returns true when the queue had to be LEAKED: a dispatch on it never
-// retired (a GPU fault or a hang), so the queue, its signal, its argument
-// slots and error slot -- and, the caller's part, the scalar staging buffer
-// and result word that dispatch reads and writes -- are kept rather than
-// freed under a running kernel.  The reason is reported on stderr once per
-// leak and the queue moves from g_live_queues to g_leaked_queues.
-// Every thread's drop-in service, for the process-exit handler: a service
-// still polling when the runtime unmaps the process's memory at exit would
-// fault on its mailbox, so exit() first stops each one and waits (200 ms at
-// most) for it to store its token -- host memory only, no HSA call (the
-// runtime may be half torn down by then).  Registered on first launch (after
-// HIP's own exit handlers, so it runs before them).
-std::mutex g_svc_mu;
-std::vector<AqlOne *> g_svc_reg;
-std::atomic<uint32_t> g_svc_tokens{0};
-std::atomic<int> g_svc_owners{0};  // threads holding a service slot (svc_allowed)
-void svc_atexit() {
-  std::lock_guard<std::mutex> lk(g_svc_mu);
-  for (AqlOne *o : g_svc_reg) {
-    if (!o->svc_live || !o->svc_out || !o->mbox || o->svc_out[6] == o->svc_token) continue;
-    mbox_post(*o, 0x80000000u | ((o->mbox_seq + 1u) & 0xffffu));
-    const double t0 = mono_s();
-    while (o->svc_out[6] != o->svc_token && mono_s() - t0 < 0.2) {
-    }
-    if (o->svc_out[6] != o->svc_token)
-      fprintf(stderr, "libmicksum: at exit, a drop-in service did not stop within 200 ms (a thread still "
-              "inside a drop-in call when exit() ran is not supported)\n");
-    o->svc_live = false;
-  }
-}
-void svc_register(AqlOne &o) {
-  if (o.svc_registered) return;
-  std::lock_guard<std::mutex> lk(g_svc_mu);
-  static const bool once = atexit(svc_atexit) == 0;
-  (void)once;
-  g_svc_reg.push_back(&o);
-  o.svc_registered = true;
-}
-void svc_unregister(AqlOne &o) {
-  if (!o.svc_registered) return;
-  std::lock_guard<std::mutex> lk(g_svc_mu);
-  g_svc_reg.erase(std::remove(g_svc_reg.begin(), g_svc_reg.end(), &o), g_svc_reg.end());
-  o.svc_registered = false;
-}
-
-void mbox_free(AqlDevice *a, uint32_t *m);
-
-bool aql_one_release(AqlOne &o) {
-  bool leaked = false;
-  svc_unregister(o);
-  if (o.svc_owner) {
-    g_svc_owners.fetch_sub(1);
-    o.svc_owner = false;
-  }
-  if (o.q) {
-    if (aql_one_quiesce(o) == 0) {
-      aql_queue_destroy(o.q);
-      if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
-      dbg_mem("one-karg-free", o.karg, 0);
-      if (o.karg) (void)jhostfree(o.karg);
-      if (o.mbox && o.mbox_dev) mbox_free(o.dev, o.mbox);
-      delete o.err;
-    } else {
-      leaked = true;
-      g_live_queues.fetch_sub(1);
-      g_leaked_queues.fetch_add(1);
-      fprintf(stderr, "libmicksum: a dispatch on this thread's HSA queue never retired (%s); the queue and the "
-              "buffers it may still use are leaked, not freed\n", t_err);
-    }
-  } else {
-    delete o.err;
-  }
-  o.device = -1;
-  o.dev = nullptr;
-  o.q = nullptr;
-  o.sig = hsa_signal_t{};
-  o.karg = nullptr;
-  o.next = 0;
-  o.unretired = false;
-  o.err = nullptr;
-  o.svc_live = false;
-  o.mbox = nullptr;
-  o.mbox_dev = false;
-  o.mbox_seq = 0;
-  o.svc_out = nullptr;
-  return leaked;
-}
-
-// Thread exit: a thread that used the library gives back its HSA queue,
-// signal, argument slots, streams and buffers (a pthread key destructor --
-// these run when a thread ends, not for the main thread at process exit,
-// when the runtime is being torn down anyway).
-// Retire the thread's drop-in dispatches before anything they use is freed;
-// if one never retires, its staging buffer and result word are leaked with
-// its queue (ctx_release then skips them).
-bool retire_dropins() {
-  if (!aql_one_release(t_aql1)) return false;
-  t_ctx.stage = t_ctx.stage_dev = nullptr;
-  t_ctx.stage_cap = 0;
-  t_ctx.sout = t_ctx.sout_dev = nullptr;
-  return true;
-}
-
-void thread_exit_cleanup(void *) {
-  retire_dropins();
-  if (t_ctx.device != -1) {
-    ctx_release(t_ctx, t_ctx.device);
-    t_ctx = ThreadCtx();
-  }
-}
-void thread_exit_register() {
-  static pthread_key_t key;
-  static const bool ok = pthread_key_create(&key, thread_exit_cleanup) == 0;
-  if (ok && !pthread_getspecific(key)) (void)pthread_setspecific(key, (void *)1);
-}
-
-// nargs explicit argument bytes at args (laid out like the kernel's
-// parameters); wait: spin on the completion signal (else the kernel signals
-// the caller itself, e.g. through a pinned host word); signal: give the
-// dispatch the completion signal without waiting (the drop-in service, whose
-// retirement the caller watches).  A running drop-in service is stopped first:
-// the packet behind it would wait for it (barrier bit).
-// A drop-in service mailbox in the GPU's fine-grained device memory that the
-// CPU may write (through the PCIe BAR): the service then polls its own HBM
-// instead of host memory over PCIe (in_cksum_hdr 2.9 us per call against 5.0
-// with the host mailbox).  (On the MI355X boxes the plain fine-grained VRAM
-// pool is never CPU-accessible; the extended-scope fine-grained one is, once
-// allowed: tools/pool_probe.cpp, profiles/r04/pool_probe_r04.jsonl.)
-// Two whole-suite GPU runs with per-thread device mailboxes allocated and
-// freed ended in an illegal-address fault reported by HIP several tests
-// later, while the same suite with host mailboxes did not fault
-// (profiles/r04/gpu_tests_*): the mailboxes now come from one slab per device
-// that is never freed (threads return their slot), which removes the
-// allocate/free churn of CPU-mapped VRAM, and the whole suite ran green with
-// it.  MI_CKSUM_DROPIN_MAILBOX=host: page-locked host memory (also the
-// fallback, nullptr here, when the platform maps no VRAM for the CPU).
+// The slot slab: fine-grained device memory the CPU may write (through the
+// PCIe BAR) -- the service then polls its own HBM instead of host memory over
+// PCIe (in_cksum_hdr 2.9 us per call against 5.0 with host mailboxes,
+// profiles/r04/dropin_breakdown_*).  On the MI355X boxes the plain
+// fine-grained VRAM pool is never CPU-accessible; the extended-scope
+// fine-grained one is, once allowed (tools/pool_probe.cpp,
+// profiles/r04/pool_probe_r04.jsonl).  One slab per device, allocated once and
+// never freed.  MI_CKSUM_DROPIN_MAILBOX=host, or no such pool: coherent
+// page-locked host memory.
 hsa_status_t mbox_cpu_cb(hsa_agent_t a, void *data) {
   hsa_device_type_t t;
   if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
@@ -3412,101 +3302,297 @@ hsa_status_t mbox_pool_cb(hsa_amd_memory_pool_t pool, void *data) {
   a->mbox_ok = true;
   return HSA_STATUS_INFO_BREAK;
 }
-constexpr uint32_t kMboxSlots = 64;
-uint32_t *mbox_alloc(AqlDevice *a) {
-  std::lock_guard<std::mutex> lk(g_aql_mu);
-  if (!a->mbox_tried) {
-    a->mbox_tried = true;
-    const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
-    void *p = nullptr;
-    if (!(e && !strcmp(e, "host")) && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK &&
-        hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a) == HSA_STATUS_INFO_BREAK && a->mbox_ok &&
-        hsa_amd_memory_pool_allocate(a->mbox_pool, 4096u * kMboxSlots, 0, &p) == HSA_STATUS_SUCCESS && p) {
-      if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
-        a->mbox_slab = (uint8_t *)p;
-        dbg_mem("mbox-slab", p, 4096u * kMboxSlots);
-      } else {
-        (void)hsa_amd_memory_pool_free(p);
-      }
+constexpr size_t kSlabBytes = 4ull * kSvcSlotWords * (kSvcSlots + 1);
+int slab_alloc(AqlDevice *a) {
+  const char *e = getenv("MI_CKSUM_DROPIN_MAILBOX");
+  void *p = nullptr;
+  if (!(e && !strcmp(e, "host")) && hsa_iterate_agents(mbox_cpu_cb, &a->cpu) == HSA_STATUS_INFO_BREAK &&
+      hsa_amd_agent_iterate_memory_pools(a->agent, mbox_pool_cb, a) == HSA_STATUS_INFO_BREAK && a->mbox_ok &&
+      hsa_amd_memory_pool_allocate(a->mbox_pool, kSlabBytes, 0, &p) == HSA_STATUS_SUCCESS && p) {
+    if (hsa_amd_agents_allow_access(1, &a->cpu, nullptr, p) == HSA_STATUS_SUCCESS) {
+      a->slab = a->slab_dev = (uint32_t *)p;
+      a->slab_vram = true;
+    } else {
+      (void)hsa_amd_memory_pool_free(p);
     }
   }
-  if (!a->mbox_slab || !~a->mbox_used) return nullptr;
-  const uint32_t k = (uint32_t)__builtin_ctzll(~a->mbox_used);
-  a->mbox_used |= 1ull << k;
-  volatile uint32_t *w = (volatile uint32_t *)(a->mbox_slab + 4096u * k);
-  for (uint32_t j = 0; j < kSvcWords; ++j) w[j] = 0u;
-  _mm_sfence();
-  return (uint32_t *)w;
-}
-// A thread's slot back to its device's slab (the slab itself is never freed).
-void mbox_free(AqlDevice *a, uint32_t *m) {
-  std::lock_guard<std::mutex> lk(g_aql_mu);
-  const uint64_t k = ((uint8_t *)m - a->mbox_slab) / 4096u;
-  if (a->mbox_slab && k < kMboxSlots) a->mbox_used &= ~(1ull << k);
-}
-
-// The thread's queue on its current device (created on first use).
-int aql_one_open(AqlOne &o) {
-  if (o.device != t_ctx.device) {
-    if (aql_one_release(o)) return set_err(-EIO, "AQL engine: the thread's previous queue never retired");
-    int rc = aql_device(t_ctx.device, &o.dev);
-    if (rc) return rc;
-    o.err = new std::atomic<int>(0);
-    if ((rc = aql_queue_create(o.dev->agent, 64, o.err, &o.q))) return rc;
-    if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
-      aql_one_release(o);
-      return set_err(-EIO, "AQL engine: hsa_signal_create failed");
+  if (!a->slab) {
+    if (jhostmalloc((void **)&a->slab, kSlabBytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&a->slab_dev, a->slab, 0) != hipSuccess) {
+      a->slab = a->slab_dev = nullptr;
+      return set_err(-ENOMEM, "drop-in service: mailbox slab");
     }
-    if (jhostmalloc((void **)&o.karg, 512 * kAqlOneSlots, hipHostMallocMapped | hipHostMallocCoherent) !=
-        hipSuccess) {
-      o.karg = nullptr;
-      aql_one_release(o);
-      return set_err(-ENOMEM, "AQL engine: kernel-argument slots");
-    }
-    dbg_mem("one-karg", o.karg, 512 * kAqlOneSlots);
-    o.device = t_ctx.device;
-    thread_exit_register();
   }
+  volatile uint32_t *w = a->slab;
+  for (size_t j = 0; j < kSlabBytes / 4; ++j) w[j] = 0u;
+  if (a->slab_vram) _mm_sfence();
+  dbg_mem("mbox-slab", a->slab_dev, kSlabBytes);
   return 0;
 }
-int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait,
-                   bool signal = false) {
-  AqlOne &o = t_aql1;
-  if (o.svc_live) {
-    int rc = svc_stop(o);
-    if (rc) return rc;
+
+// The device's drop-in queue, the service's completion signal, argument block
+// and exit word, and the slab (created once, on first use).
+int dq_open(AqlDevice *a) {
+  std::lock_guard<std::mutex> lk(a->dq_mu);
+  if (a->dq) return 0;
+  if (a->dq_rc) return set_err(a->dq_rc, "AQL engine: the drop-in queue could not be set up");
+  hsa_queue_t *q = nullptr, *sq = nullptr;
+  int rc = aql_queue_create(a->agent, 256, &a->dq_err, &q);
+  if (!rc) rc = aql_queue_create(a->agent, 64, &a->dq_err, &sq);
+  if (!rc && hsa_signal_create(0, 0, nullptr, &a->svc_sig) != HSA_STATUS_SUCCESS)
+    rc = set_err(-EIO, "AQL engine: hsa_signal_create failed");
+  if (!rc && jhostmalloc((void **)&a->svc_karg, 512, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+    rc = set_err(-ENOMEM, "drop-in service: kernel-argument block");
+  if (!rc && (jhostmalloc((void **)&a->svc_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+              hipHostGetDevicePointer((void **)&a->svc_host_dev, (void *)a->svc_host, 0) != hipSuccess))
+    rc = set_err(-ENOMEM, "drop-in service: exit word");
+  if (!rc) rc = slab_alloc(a);
+  if (rc) {
+    a->dq_rc = rc;
+    aql_queue_destroy(q);
+    aql_queue_destroy(sq);
+    return rc;
   }
-  int rc = aql_one_open(o);
-  if (rc) return rc;
-  const AqlKernel &k = o.dev->k[id];
+  a->svc_host[0] = 0;
+  a->sq = sq;
+  a->dq = q;
+  return 0;
+}
+
+// One dispatch packet into the device's drop-in queue.  The kernel arguments
+// go into `ka` (the caller's block, not in use by an earlier dispatch); no
+// barrier bit; system-scope fences both ways (the kernels read host memory the
+// host rewrites every call and write host memory).
+int dq_dispatch_locked(AqlDevice *a, hsa_queue_t *q, int id, unsigned blocks, unsigned wg, const void *args,
+                       uint32_t nargs, uint8_t *ka, hsa_signal_t sig) {
+  const AqlKernel &k = a->k[id];
   if (k.kernarg > 512u) return set_err(-EPROTO, "AQL engine: kernarg segment %u B", k.kernarg);
-  uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
   memset(ka, 0, k.kernarg);
   aql_fill_raw(ka, args, nargs, blocks, wg, k.kernarg);
   hsa_kernel_dispatch_packet_t t;
   aql_fill_packet(t, k, blocks, ka, wg);
-  uint64_t idx;
-  void *p;
-  if ((rc = aql_one_slot(o, &idx, &p))) return rc;
-  hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)p;
+  const uint64_t idx = hsa_queue_add_write_index_screlease(q, 1);
+  const double t0 = mono_s();
+  while (idx - hsa_queue_load_read_index_scacquire(q) >= q->size) {
+    if (a->dq_err.load()) return set_err(-EIO, "AQL engine: drop-in queue error 0x%x", a->dq_err.load());
+    if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "AQL engine: drop-in queue full for 10 s");
+  }
+  hsa_kernel_dispatch_packet_t *slot = (hsa_kernel_dispatch_packet_t *)q->base_address + (idx & (q->size - 1));
   memcpy((uint8_t *)slot + 4, (const uint8_t *)&t + 4, sizeof t - 4);
-  const bool sig = wait || signal;
-  if (sig) hsa_signal_store_relaxed(o.sig, 1);
-  slot->completion_signal = sig ? o.sig : hsa_signal_t{0};
-  // system-scope fences both ways: the kernels read host memory the host
-  // rewrites every call (burst, staging, descriptors) and write host memory
+  slot->completion_signal = sig;
   const uint32_t sc = HSA_FENCE_SCOPE_SYSTEM;
-  const uint32_t hs = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) | (1u << HSA_PACKET_HEADER_BARRIER) |
+  const uint32_t hs = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
                       (sc << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) | (sc << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE) |
                       ((uint32_t)t.setup << 16);
   __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
-  hsa_signal_store_screlease(o.q->doorbell_signal, (hsa_signal_value_t)idx);
-  if (t_dtrace.on) t_dtrace.t_doorbell = sys_ts();
-  if (!wait) {
-    o.unretired = true;
-    return 0;
+  hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)idx);
+  return 0;
+}
+
+// The service's exit at process exit: a service still polling when the runtime
+// unmaps the process's memory would fault on the slab, so exit() moves every
+// device's control word and waits (200 ms at most) for the running service to
+// store its launch token -- memory stores and loads only, no HSA call (the
+// runtime may be half torn down by then).  The control word is written by
+// nobody else but mi__set_dropin_service(0), under the same lock; a thread
+// still inside a drop-in when exit() runs finds its service gone (and would
+// relaunch it): that is not supported, and reported.  Registered on the first
+// launch, after HIP's own exit handlers, so it runs before them.
+std::atomic<uint32_t> g_svc_tokens{0};
+void svc_stop_locked(AqlDevice *a, double timeout_s) {
+  if (!a->svc_launched.load() || a->svc_host[0] == a->svc_token) return;
+  volatile uint32_t *ctl = a->slab + (size_t)kSvcSlots * kSvcSlotWords;
+  if (a->slab_vram) _mm_sfence();
+  *ctl = ++a->ctl;
+  if (a->slab_vram) _mm_sfence();
+  const double t0 = mono_s();
+  while (a->svc_host[0] != a->svc_token && mono_s() - t0 < timeout_s) {
   }
-  return aql_one_wait(o);
+  if (a->svc_host[0] != a->svc_token)
+    fprintf(stderr, "libmicksum: the drop-in service did not stop within %.0f ms\n", timeout_s * 1e3);
+}
+void svc_atexit() {
+  for (AqlDevice &a : g_aql) {
+    if (!a.dq) continue;
+    std::unique_lock<std::mutex> lk(a.dq_mu, std::try_to_lock);  // (a thread mid-call may hold it)
+    svc_stop_locked(&a, 0.2);
+  }
+}
+
+// The drop-in service switch (on by default; MI_CKSUM_DROPIN_SERVICE=0 or
+// mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
+// (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
+// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
+// in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
+// mailbox) against 8.1 us for a dispatch per call.
+std::atomic<int> g_dropin_svc{-1};
+bool dropin_svc_on() {
+  int v = g_dropin_svc.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE");
+    v = e && e[0] == '0' ? 0 : 1;
+    g_dropin_svc.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+// (diagnostics: mi__set_dropin_service_params overrides both for later launches)
+std::atomic<uint32_t> g_svc_idle_us{0}, g_svc_poll{1};
+uint32_t dropin_svc_idle_ticks() {
+  if (const uint32_t us = g_svc_idle_us.load()) return us * 100u;
+  static const uint32_t t = [] {
+    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_IDLE_US");
+    const long us = e ? atol(e) : 0;
+    return (uint32_t)((us > 0 && us < 10000000 ? us : 1000) * 100);  // the 100 MHz clock
+  }();
+  return t;
+}
+
+// The device's service running: launch it when it never ran or has retired
+// (its idle exit, a stop).  The fast path reads two words; the launch is under
+// the queue's lock, and re-checks, so two threads that both saw it retire
+// launch it once.
+int svc_ensure(AqlDevice *a) {
+  if (a->svc_launched.load(std::memory_order_acquire) && hsa_signal_load_relaxed(a->svc_sig) != 0) return 0;
+  std::lock_guard<std::mutex> lk(a->dq_mu);
+  if (a->svc_launched.load() && hsa_signal_load_scacquire(a->svc_sig) != 0) return 0;
+  static const bool once = atexit(svc_atexit) == 0;
+  (void)once;
+  struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
+    const uint32_t *slab;
+    uint32_t nslots;
+    uint32_t *exitw;
+    uint32_t token, idle_ticks;
+  };
+  static_assert(sizeof(SvcArgs) == 32, "kernel-argument layout of mi_aql_dropin_svc");
+  const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
+  const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8), a->svc_host_dev, token, dropin_svc_idle_ticks()};
+  hsa_signal_store_relaxed(a->svc_sig, 1);
+  int rc = dq_dispatch_locked(a, a->sq, kAqlSvc, 1, kScalarThreads, &s, sizeof s, a->svc_karg, a->svc_sig);
+  if (rc) {
+    hsa_signal_store_relaxed(a->svc_sig, 0);
+    return rc;
+  }
+  a->svc_token = token;
+  a->svc_launched.store(true, std::memory_order_release);
+  return 0;
+}
+
+// A mailbox slot for the thread (-1: all kSvcSlots taken -- the call then
+// dispatches), and back.
+int slot_take(AqlDevice *a) {
+  std::lock_guard<std::mutex> lk(a->dq_mu);
+  const uint64_t free = ~a->slot_used & ((1ull << kSvcSlots) - 1u);
+  if (!free) return -1;
+  const int k = __builtin_ctzll(free);
+  a->slot_used |= 1ull << k;
+  return k;
+}
+void slot_give(AqlDevice *a, int k) {
+  std::lock_guard<std::mutex> lk(a->dq_mu);
+  a->slot_used &= ~(1ull << k);
+}
+
+// Returns true when the thread's dispatch state had to be LEAKED (stuck: a
+// dispatch or request never finished, so its argument blocks, signal and
+// slot -- and, the caller's part, the staging buffer and result block -- are
+// kept rather than freed under a kernel that may still run; reported on
+// stderr once).
+bool aql_one_release(AqlOne &o) {
+  const bool leaked = o.stuck;
+  if (leaked) {
+    fprintf(stderr, "libmicksum: a drop-in or burst of this thread never finished (%s); its argument blocks, "
+            "signal, mailbox slot and buffers are leaked, not freed\n", t_err);
+  } else {
+    if (o.slot >= 0) slot_give(o.dev, o.slot);
+    if (o.sig.handle) (void)hsa_signal_destroy(o.sig);
+    dbg_mem("one-karg-free", o.karg, 0);
+    if (o.karg) (void)jhostfree(o.karg);
+  }
+  o = AqlOne();
+  return leaked;
+}
+
+// Thread exit: a thread that used the library gives back its signal,
+// argument blocks, slot, streams and buffers (a pthread key destructor --
+// these run when a thread ends, not for the main thread at process exit, when
+// the runtime is being torn down anyway).  If the thread is stuck, its
+// staging buffer and result block are leaked with the rest (ctx_release then
+// skips them).
+bool retire_dropins() {
+  if (!aql_one_release(t_aql1)) return false;
+  t_ctx.stage = t_ctx.stage_dev = nullptr;
+  t_ctx.stage_cap = 0;
+  t_ctx.sout = t_ctx.sout_dev = nullptr;
+  return true;
+}
+
+void thread_exit_cleanup(void *) {
+  retire_dropins();
+  if (t_ctx.device != -1) {
+    ctx_release(t_ctx, t_ctx.device);
+    t_ctx = ThreadCtx();
+  }
+}
+void thread_exit_register() {
+  static pthread_key_t key;
+  static const bool ok = pthread_key_create(&key, thread_exit_cleanup) == 0;
+  if (ok && !pthread_getspecific(key)) (void)pthread_setspecific(key, (void *)1);
+}
+
+// The thread's dispatch state on its current device (created on first use).
+int aql_one_open(AqlOne &o) {
+  if (o.device == t_ctx.device) return 0;
+  if (aql_one_release(o)) return set_err(-EIO, "AQL engine: the thread's previous dispatch never finished");
+  int rc = aql_device(t_ctx.device, &o.dev);
+  if (rc || (rc = dq_open(o.dev))) {
+    o.dev = nullptr;
+    return rc;
+  }
+  if (hsa_signal_create(0, 0, nullptr, &o.sig) != HSA_STATUS_SUCCESS) {
+    o = AqlOne();
+    return set_err(-EIO, "AQL engine: hsa_signal_create failed");
+  }
+  if (jhostmalloc((void **)&o.karg, 512 * kAqlOneSlots, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    (void)hsa_signal_destroy(o.sig);
+    o = AqlOne();
+    return set_err(-ENOMEM, "AQL engine: kernel-argument slots");
+  }
+  dbg_mem("one-karg", o.karg, 512 * kAqlOneSlots);
+  o.device = t_ctx.device;
+  thread_exit_register();
+  return 0;
+}
+// Spin (deadline-bounded) until the thread's signal reads 0.
+int aql_one_wait(AqlOne &o) {
+  const double t0 = mono_s();
+  while (hsa_signal_wait_scacquire(o.sig, HSA_SIGNAL_CONDITION_EQ, 0, 1000000, HSA_WAIT_STATE_ACTIVE) != 0) {
+    if (o.dev->dq_err.load()) {
+      o.stuck = true;
+      return set_err(-EIO, "AQL engine: drop-in queue error 0x%x", o.dev->dq_err.load());
+    }
+    if (mono_s() - t0 > kAqlDeadline) {
+      o.stuck = true;
+      return set_err(-ETIMEDOUT, "AQL engine: dispatch not complete after 10 s");
+    }
+  }
+  return 0;
+}
+// nargs explicit argument bytes at args (laid out like the kernel's
+// parameters); wait: the packet carries the thread's signal and the call spins
+// on it (else the kernel signals the caller itself, through a pinned word).
+int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint32_t nargs, bool wait) {
+  AqlOne &o = t_aql1;
+  int rc = aql_one_open(o);
+  if (rc) return rc;
+  uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
+  if (wait) hsa_signal_store_relaxed(o.sig, 1);
+  {
+    std::lock_guard<std::mutex> lk(o.dev->dq_mu);
+    rc = dq_dispatch_locked(o.dev, o.dev->dq, id, blocks, wg, args, nargs, ka, wait ? o.sig : hsa_signal_t{0});
+  }
+  if (rc) return rc;
+  if (t_dtrace.on) t_dtrace.t_doorbell = sys_ts();
+  return wait ? aql_one_wait(o) : 0;
 }
 
 }  // namespace
@@ -4353,105 +4439,65 @@ int mi_cksum_host_unregister(void *p) {
   return 0;
 }
 
-// The drop-in service switch (on by default; MI_CKSUM_DROPIN_SERVICE=0 or
-// mi__set_dropin_service(0): one AQL dispatch per call) and its idle exit
-// (MI_CKSUM_DROPIN_SERVICE_IDLE_US, default 1000 us).  Measured on the MI355X
-// host (tools/dropin_breakdown.py, profiles/r04/dropin_breakdown_*.jsonl):
-// in_cksum_hdr 2.9 us per call with the VRAM mailbox (5.0 with the host
-// mailbox) against 8.1 us for a dispatch per call.
-std::atomic<int> g_dropin_svc{-1};
-// At most MI_CKSUM_DROPIN_SERVICE_MAX (default 8) threads of the process run
-// a drop-in service at once: each is a resident 512-lane workgroup polling
-// its thread's own HSA queue, and more of them than the hardware maps queues
-// for would be time-sliced by the command processor.  A thread
-// takes a slot with its first service call and gives it back when its queue is
-// released (thread exit, device switch); threads beyond the cap keep one
-// dispatch per call.
-int dropin_svc_max() {
-  static const int m = [] {
-    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_MAX");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 8;
-  }();
-  return m;
-}
-bool svc_allowed(AqlOne &o) {
-  if (o.svc_owner) return true;
-  if (g_svc_owners.fetch_add(1) >= dropin_svc_max()) {
-    g_svc_owners.fetch_sub(1);
-    return false;
-  }
-  o.svc_owner = true;
-  return true;
-}
-bool dropin_svc_on() {
-  int v = g_dropin_svc.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE");
-    v = e && e[0] == '0' ? 0 : 1;
-    g_dropin_svc.store(v, std::memory_order_relaxed);
-  }
-  return v == 1;
-}
-uint32_t dropin_svc_idle_ticks() {
-  static const uint32_t t = [] {
-    const char *e = getenv("MI_CKSUM_DROPIN_SERVICE_IDLE_US");
-    const long us = e ? atol(e) : 0;
-    return (uint32_t)((us > 0 && us < 10000000 ? us : 1000) * 100);  // the 100 MHz clock
-  }();
-  return t;
-}
-
 // The service machinery shared by the (b1) drop-ins (mi__scalar_fold) and the
-// small host RX bursts (verify_host_zero_copy): the thread's queue, its
-// mailbox and result block, (re)launch, one request and its result word.
-struct SvcArgs {  // mi_aql_dropin_svc's parameters, in order
-  const uint8_t *base;
-  uint32_t bytes, token;
-  const uint32_t *box;
-  uint32_t *out;
-  uint32_t seq0, idle_ticks;
-};
-static_assert(sizeof(SvcArgs) == 40, "kernel-argument layout of mi_aql_dropin_svc");
+// small host RX bursts (verify_host_zero_copy): the thread's result block, its
+// slot, one request and its result word.
 static int ensure_sout(ThreadCtx &c) {
   if (c.sout) return 0;
-  // words 0..5: the result and the trace stamps; 16..: the service mailbox
-  // when it lives in host memory
+  // words 0..5: the result and the trace stamps (kOutWords)
   HIP_TRY(jhostmalloc((void **)&c.sout, 4096, hipHostMallocMapped | hipHostMallocCoherent));
   HIP_TRY(hipHostGetDevicePointer((void **)&c.sout_dev, c.sout, 0));
   memset(c.sout, 0, 4096);
   dbg_mem("sout", c.sout_dev, 4096);
   return 0;
 }
+// The thread's slot, its header current (result block, staging buffer):
+// 0 ready, 1 no slot free (the call dispatches instead), < 0 an error.
 static int svc_open(ThreadCtx &c, AqlOne &o) {
   int rc = ensure_sout(c);
   if (rc || (rc = aql_one_open(o))) return rc;
-  if (!o.mbox) {
-    uint32_t *m = mbox_alloc(o.dev);
-    o.mbox_dev = m != nullptr;
-    o.mbox = m ? m : c.sout + 16;
-    o.mbox_seq = 0;
+  if (o.slot < 0 && (o.slot = slot_take(o.dev)) < 0) return 1;
+  const uint64_t out = (uint64_t)c.sout_dev, stg = (uint64_t)c.stage_dev;
+  if (o.hdr_out != out || o.hdr_stage != stg || o.hdr_bytes != (uint32_t)c.stage_cap) {
+    volatile uint32_t *w = o.dev->slab + (size_t)o.slot * kSvcSlotWords;
+    w[kBoxStageBytes] = (uint32_t)c.stage_cap;
+    w[kBoxOut] = (uint32_t)out;
+    w[kBoxOut + 1] = (uint32_t)(out >> 32);
+    w[kBoxStage] = (uint32_t)stg;
+    w[kBoxStage + 1] = (uint32_t)(stg >> 32);
+    o.hdr_out = out;
+    o.hdr_stage = stg;
+    o.hdr_bytes = (uint32_t)c.stage_cap;
   }
   return 0;
 }
-// the mailbox as the GPU addresses it
-static uint32_t *svc_box_dev(ThreadCtx &c, AqlOne &o) { return o.mbox_dev ? o.mbox : c.sout_dev + 16; }
-// (re)start the service: it serves any sequence word other than seq0
-static int svc_launch(ThreadCtx &c, AqlOne &o, uint32_t seq0) {
-  const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
-  const SvcArgs a{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, token, svc_box_dev(c, o), c.sout_dev, seq0,
-                  dropin_svc_idle_ticks()};
-  int r = aql_one_submit(kAqlSvc, 1, kScalarThreads, &a, sizeof a, false, true);
-  if (r) return r;
-  o.svc_token = token;
-  o.svc_out = c.sout;
-  svc_register(o);
-  o.svc_live = true;
-  return 0;
+// the slot, host view
+static volatile uint32_t *svc_box(AqlOne &o) { return o.dev->slab + (size_t)o.slot * kSvcSlotWords; }
+static const uint32_t *svc_box_dev(AqlOne &o) { return o.dev->slab_dev + (size_t)o.slot * kSvcSlotWords; }
+// Post a request (fields and inline bytes already written): the sequence word
+// last -- flags | the call's tag, never the slot's previous word (a slot
+// changes owners; each owner's tags run on their own) -- and the service
+// running.  A VRAM slab is write-combined BAR memory, hence the store fences.
+// Returns the tag the result word will carry.
+static int svc_post(ThreadCtx &c, AqlOne &o, uint32_t flags, uint32_t tag, uint32_t *tag_out) {
+  AqlDevice *a = o.dev;
+  uint32_t seq = flags | tag;
+  if (seq == a->slot_seq[o.slot]) {
+    tag = next_tag(c);
+    seq = flags | tag;
+  }
+  volatile uint32_t *w = svc_box(o);
+  if (a->slab_vram) _mm_sfence();
+  __atomic_store_n((uint32_t *)&w[kBoxSeq], seq, __ATOMIC_RELEASE);
+  if (a->slab_vram) _mm_sfence();
+  a->slot_seq[o.slot] = seq;
+  *tag_out = tag;
+  return svc_ensure(a);
 }
 // Spin on the result word for `tag`; relaunch the service if it retired
-// (idle exit) before serving the request posted after `prev`.
-static int svc_wait(ThreadCtx &c, AqlOne &o, uint32_t tag, uint32_t prev, uint32_t *word) {
+// (idle exit, a stop) -- the new one starts from the slots' acknowledged
+// words, so it serves a request the old one left behind.
+static int svc_wait(ThreadCtx &c, AqlOne &o, uint32_t tag, uint32_t *word) {
   volatile uint32_t *slot = c.sout;
   const double t0 = mono_s();
   for (uint32_t polls = 1;; ++polls) {
@@ -4461,21 +4507,16 @@ static int svc_wait(ThreadCtx &c, AqlOne &o, uint32_t tag, uint32_t prev, uint32
       return 0;
     }
     if ((polls & 255u) == 0) {
-      if (o.error()) return set_err(-EIO, "drop-in service: queue error 0x%x", o.error());
-      const bool retired = hsa_signal_load_scacquire(o.sig) == 0;
-      v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);  // (the store and the completion race)
-      if ((v >> 16) == tag) {
-        *word = v;
-        return 0;
+      if (o.dev->dq_err.load()) {
+        o.stuck = true;
+        return set_err(-EIO, "drop-in service: queue error 0x%x", o.dev->dq_err.load());
       }
-      if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "drop-in service: no result after 10 s");
-      if (retired) {
-        // the service took its idle exit before this request: a new one
-        o.svc_live = false;
-        o.unretired = false;
-        int rc = svc_launch(c, o, prev);
-        if (rc) return rc;
+      if (mono_s() - t0 > kAqlDeadline) {
+        o.stuck = true;
+        return set_err(-ETIMEDOUT, "drop-in service: no result after 10 s");
       }
+      int rc = svc_ensure(o.dev);
+      if (rc) return rc;
     }
   }
 }
@@ -4495,6 +4536,7 @@ struct HostOut {
 
 static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, const HostOut &o,
                                  uint32_t *bad_count) {
+  if (t_dtrace.on) t_dtrace.t_entry = sys_ts();
   ThreadCtx &c = t_ctx;
   const uint64_t n = b->n;
   // Descriptors and outputs go through one page-locked, mapped, coherent host
@@ -4582,12 +4624,14 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     const long v = e ? atol(e) : 64L;
     return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
   }();
-  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0 && svc_allowed(t_aql1)) {
+  int svc = 1;  // 0: the burst goes to the service
+  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0 &&
+      (svc = svc_open(c, t_aql1)) < 0)
+    return svc;
+  if (svc == 0) {
     AqlOne &o = t_aql1;
-    int rc = svc_open(c, o);
-    if (rc) return rc;
-    uint8_t *inl = (uint8_t *)(o.mbox + kSvcInline);                  // host view
-    const uint8_t *inl_dev = (const uint8_t *)(svc_box_dev(c, o) + kSvcInline);  // the GPU's
+    uint8_t *inl = (uint8_t *)(svc_box(o) + kSvcInline);                  // host view
+    const uint8_t *inl_dev = (const uint8_t *)(svc_box_dev(o) + kSvcInline);  // the GPU's
     BurstArgs a{};
     a.d = d;
     size_t at = 128;  // the arguments, then offsets and lengths
@@ -4606,11 +4650,29 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     a.st = zst;
     a.bad = nullptr;
     memcpy(inl, &a, sizeof a);
-    const uint32_t tag = next_tag(c), prev = o.mbox_seq;
-    if (!o.svc_live && (rc = svc_launch(c, o, prev))) return rc;
-    mbox_post(o, 0x40000000u | (((uint32_t)(sizeof a + 15u) >> 4) << 16) | tag);  // bit 30: a burst
-    uint32_t w;
-    if ((rc = svc_wait(c, o, tag, prev, &w))) return rc;
+    static const uint32_t fences = [] {  // diagnostics only: see the service kernel
+      const char *e = getenv("MI_CKSUM_BURST_FENCES");
+      return e ? (uint32_t)atoi(e) & 3u : 0u;
+    }();
+    volatile uint32_t *bx = svc_box(o);
+    bx[2] = fences;
+    bx[10] = t_dtrace.on ? 1u : 0u;
+    if (t_dtrace.on) memset(c.sout + 1, 0, 28);
+    uint32_t tag = 0, w = 0;
+    int rc = svc_post(c, o, 0x40000000u | (((uint32_t)(sizeof a + 15u) >> 4) << 16), next_tag(c), &tag);  // bit 30: a burst
+    if (t_dtrace.on) t_dtrace.t_doorbell = sys_ts();
+    if (rc || (rc = svc_wait(c, o, tag, &w))) return rc;
+    if (t_dtrace.on) {
+      t_dtrace.t_seen = sys_ts();
+      uint64_t k0 = 0, k1 = 0;
+      memcpy(&k0, (const void *)(c.sout + 2), 8);
+      memcpy(&k1, (const void *)(c.sout + 4), 8);
+      t_dtrace.g_start = k0;
+      t_dtrace.g_end = k1 >= k0 ? k1 : k0;
+      t_dtrace.b_acq = c.sout[1];
+      t_dtrace.b_body = c.sout[6];
+      t_dtrace.b_rel = c.sout[7];
+    }
   } else if (host_aql && aql_device(t_ctx.device, &adv) == 0 &&
       (wide ? aql_kernel_for_shape(d, Shape{64, 4}, &id, &blocks)
                         : aql_kernel_for(d, max_len, &id, &blocks)) == 0) {
@@ -4925,14 +4987,14 @@ uint8_t *mi__scalar_staging(size_t need) {
   ThreadCtx &c = t_ctx;
   if (need < 4096) need = 4096;
   if (c.stage_cap < need) {
-    // the thread's last scalar dispatch may still be retiring: it must be done
-    // with the old buffer before it is freed
-    if (aql_one_quiesce(t_aql1)) return nullptr;
+    // (every drop-in kernel has read the buffer before storing its result, so
+    // once a call has returned nothing reads it -- unless a call failed
+    // without its result: then the old buffer is leaked, not freed)
     if (c.sstream && hipStreamSynchronize(c.sstream) != hipSuccess) {
       set_err(-EIO, "scalar staging: stream");
       return nullptr;
     }
-    if (c.stage) {
+    if (c.stage && !t_aql1.stuck) {
       dbg_mem("stage-free", c.stage_dev, 0);
       (void)jhostfree(c.stage);
     }
@@ -4989,13 +5051,12 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   }();
   AqlDevice *adv = nullptr;
   const bool aql = host_aql && aql_device(c.device, &adv) == 0;
-  const bool svc = aql && dropin_svc_on() && svc_allowed(t_aql1);
   AqlOne &o = t_aql1;
-  uint32_t prev = 0;
-  if (svc) {
-    if ((rc = svc_open(c, o))) return rc;
-    volatile uint32_t *bx = o.mbox;
-    prev = o.mbox_seq;
+  int svc = 1;  // 0: the service serves this call
+  if (aql && dropin_svc_on() && (svc = svc_open(c, o)) < 0) return svc;
+  uint32_t wtag = tag;
+  if (svc == 0) {
+    volatile uint32_t *bx = svc_box(o);
     const bool inl = off + len <= kSvcInlineBytes;
     const uint32_t nck = inl ? (uint32_t)(off + len + 15u) >> 4 : 0u;
     bx[2] = (uint32_t)off;
@@ -5007,11 +5068,10 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     bx[8] = proto;
     bx[9] = plen;
     bx[10] = trace ? 1u : 0u;
-    // the staging bytes [0, off + len) into the mailbox's inline area, whole
+    // the staging bytes [0, off + len) into the slot's inline area, whole
     // 16-byte chunks (the staging buffer holds at least 4 KiB)
     if (nck) memcpy((void *)(bx + kSvcInline), c.stage, 16u * nck);
-    if (!o.svc_live && (rc = svc_launch(c, o, prev))) return rc;
-    mbox_post(o, tag | (nck << 16));
+    if ((rc = svc_post(c, o, nck << 16, tag, &wtag))) return rc;
     if (trace) t_dtrace.t_doorbell = sys_ts();
   } else if (aql) {
     const ScalarArgs sa{(const uint8_t *)c.stage_dev, (uint32_t)c.stage_cap, (uint32_t)off, len,
@@ -5031,8 +5091,8 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   volatile uint32_t *slot = c.sout;
   uint32_t v = 0;
   const double t0 = mono_s();
-  if (svc) {
-    if ((rc = svc_wait(c, o, tag, prev, &v))) return rc;
+  if (svc == 0) {
+    if ((rc = svc_wait(c, o, wtag, &v))) return rc;
   } else {
     for (uint32_t polls = 1;; ++polls) {
       v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
@@ -5042,7 +5102,10 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
         // the completion race)
         bool retired = false;  // (an unsignalled AQL dispatch: only the word, the queue and the deadline tell)
         if (aql) {
-          if (o.error()) return set_err(-EIO, "scalar fold: queue error 0x%x", o.error());
+          if (o.dev->dq_err.load()) {
+            o.stuck = true;
+            return set_err(-EIO, "scalar fold: queue error 0x%x", o.dev->dq_err.load());
+          }
         } else {
           const hipError_t e = hipStreamQuery(c.sstream);
           if (e != hipSuccess && e != hipErrorNotReady) return set_err(-EIO, "scalar fold: %s", hipGetErrorString(e));
@@ -5050,7 +5113,10 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
         }
         v = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
         if ((v >> 16) == tag) break;
-        if (mono_s() - t0 > kAqlDeadline) return set_err(-ETIMEDOUT, "scalar fold: no result after 10 s");
+        if (mono_s() - t0 > kAqlDeadline) {
+          o.stuck = aql;
+          return set_err(-ETIMEDOUT, "scalar fold: no result after 10 s");
+        }
         if (retired) return set_err(-EIO, "scalar fold: the kernel ended without a result");
       }
     }
@@ -5097,22 +5163,58 @@ int mi__dropin_trace_read(double *out, int n) {
   out[1] = t.g_start ? (double)(t.g_end - t.g_start) * 0.01 : -1.0;  // 100 MHz
   out[2] = us(t.t_seen);
   out[3] = 0.0;
+  if (n >= 7) {  // a service burst: acquire done, burst done, release done (us after the request was seen)
+    out[4] = t.b_acq * 0.01;
+    out[5] = t.b_body * 0.01;
+    out[6] = t.b_rel * 0.01;
+  }
   return 0;
 }
 // Diagnostics / tests (not in the public header): the drop-in service on (1)
-// or off (0) for calls from now on; a thread's running service is stopped by
-// its next call's other path or at thread exit.  Returns the previous setting.
+// or off (0) for calls from now on; off also stops the calling thread's
+// device's service (a thread mid-call elsewhere relaunches it for that call).
+// Returns the previous setting.
 int mi__set_dropin_service(int on) {
   const int was = dropin_svc_on() ? 1 : 0;
   g_dropin_svc.store(on ? 1 : 0);
-  if (!on && t_aql1.svc_live) {
-    int rc = svc_stop(t_aql1);
-    if (rc) return rc;
+  AqlDevice *a = t_aql1.dev;
+  if (!on && a && a->dq) {
+    std::lock_guard<std::mutex> lk(a->dq_mu);
+    svc_stop_locked(a, 1.0);
   }
   return was;
 }
-// Is the calling thread's drop-in service running?  (tests)
-int mi__dropin_service_live(void) { return t_aql1.svc_live ? 1 : 0; }
+// Diagnostics (tools/service_interference.py): the service's idle exit (us;
+// 0: the default) and poll period (s_sleep units, 1-255) for launches from now on.
+void mi__set_dropin_service_params(uint32_t idle_us, uint32_t poll) {
+  g_svc_idle_us.store(idle_us < 10000000u ? idle_us : 10000000u);
+  g_svc_poll.store(poll < 1u ? 1u : poll > 255u ? 255u : poll);
+}
+// Diagnostics: a resident wave (mi_aql_spin) for `us` microseconds, launched
+// without waiting -- via 0: a HIP stream of the thread's; 1: the device's
+// service queue; 2: its dispatch queue.
+int mi__spin(uint32_t us, int via) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  const uint64_t ticks = (uint64_t)us * 100u;
+  if (via == 0) {
+    if (!t_ctx.sstream) HIP_TRY(hipStreamCreateWithFlags(&t_ctx.sstream, hipStreamNonBlocking));
+    hipLaunchKernelGGL(mi_aql_spin, dim3(1), dim3(64), 0, t_ctx.sstream, ticks);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  AqlOne &o = t_aql1;
+  if ((rc = aql_one_open(o))) return rc;
+  uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
+  std::lock_guard<std::mutex> lk(o.dev->dq_mu);
+  return dq_dispatch_locked(o.dev, via == 1 ? o.dev->sq : o.dev->dq, kAqlSpin, 1, 64, &ticks, sizeof ticks, ka,
+                            hsa_signal_t{0});
+}
+// Is the drop-in service of the calling thread's device running?  (tests)
+int mi__dropin_service_live(void) {
+  const AqlDevice *a = t_aql1.dev;
+  return a && a->svc_launched.load() && hsa_signal_load_scacquire(a->svc_sig) != 0 ? 1 : 0;
+}
 // Tests / A-B runs: dealt units for the prepared submissions on (1) or off
 // (0); returns the previous setting.  Takes effect for handles created after.
 int mi__set_deal(int on) {
@@ -5121,12 +5223,18 @@ int mi__set_deal(int on) {
   return was;
 }
 // Tests: the calling thread's last drop-in tag (the next call uses the one
-// after it), and the number of threads holding a service slot.
+// after it), and the number of threads holding a mailbox slot on the calling
+// thread's device.
 void mi__set_dropin_tag(uint32_t tag) { t_ctx.stag = tag & 0xffffu; }
-int mi__dropin_service_owners(void) { return g_svc_owners.load(); }
-// Where the calling thread's service mailbox lives: 0 none yet, 1 page-locked
+int mi__dropin_service_owners(void) {
+  AqlDevice *a = t_aql1.dev;
+  if (!a) return 0;
+  std::lock_guard<std::mutex> lk(a->dq_mu);
+  return __builtin_popcountll(a->slot_used);
+}
+// Where the calling thread's service slot lives: 0 none yet, 1 page-locked
 // host memory, 2 device memory written through the BAR.  (tests, bench)
-int mi__dropin_mailbox(void) { return !t_aql1.mbox ? 0 : t_aql1.mbox_dev ? 2 : 1; }
+int mi__dropin_mailbox(void) { return t_aql1.slot < 0 ? 0 : t_aql1.dev->slab_vram ? 2 : 1; }
 
 void mi__fatal(const char *what) {
   fprintf(stderr, "libmicksum: %s: %s\n", what, t_err[0] ? t_err : "unknown error");

@@ -51,7 +51,7 @@ def _kernels(tmp_path):
 
 def test_aql_entry_points_kernarg_layout(tmp_path):
     ks = _kernels(tmp_path)
-    verify = [k for k in ks if k not in ("mi_aql_scalar", "mi_aql_dropin_svc")]
+    verify = [k for k in ks if k not in ("mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin")]
     assert "mi_aql_v_16x6" in ks and "mi_aql_run8" in ks and "mi_aql_slot64" in ks and "mi_aql_scalar" in ks
     assert "mi_aql_vd_16x6" in ks and "mi_aql_vd_8x12" in ks
     for name in verify:
@@ -72,15 +72,15 @@ def test_aql_entry_points_kernarg_layout(tmp_path):
         for o, s, k in args:
             if k in HIDDEN:
                 assert o == SCALAR_EXPLICIT + HIDDEN[k], ("mi_aql_scalar", k, o)
-    # mi_aql_dropin_svc(base, bytes, token, box, out, seq0, idle_ticks): SvcArgs
-    # in mi__scalar_fold, 40 bytes
+    # mi_aql_dropin_svc(slab, nslots, exitw, token, idle_ticks): SvcArgs in
+    # svc_ensure, 32 bytes
     args, seg = ks["mi_aql_dropin_svc"]
     explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]
-    assert explicit == [(0, 8), (8, 4), (12, 4), (16, 8), (24, 8), (32, 4), (36, 4)], explicit
-    if seg > 40:
+    assert explicit == [(0, 8), (8, 4), (16, 8), (24, 4), (28, 4)], explicit
+    if seg > 32:
         for o, s, k in args:
             if k in HIDDEN:
-                assert o == 40 + HIDDEN[k], ("mi_aql_dropin_svc", k, o)
+                assert o == 32 + HIDDEN[k], ("mi_aql_dropin_svc", k, o)
 
 
 def _all_kernel_notes(tmp_path):

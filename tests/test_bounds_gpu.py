@@ -193,14 +193,17 @@ def test_dropin_tag_wraps_past_zero():
     assert res["dt"] < 2.0, res["dt"]
 
 
-def test_dropin_service_slots_are_capped():
-    """16 threads calling drop-ins at once: at most MI_CKSUM_DROPIN_SERVICE_MAX
-    (8) hold a service; the others keep one dispatch per call; every answer
-    right; the slots come back when the threads exit."""
+def test_dropin_threads_share_one_service():
+    """16 threads calling drop-ins at once: each holds a mailbox slot of the
+    device's ONE service (no queue per thread: the process's queue count does
+    not move), every answer right, and the slots come back when the threads
+    exit."""
     lib = _lib()
     was = lib.mi__set_dropin_service(1)
+    assert mi.in_cksum_hdr(KAT_HDR) == 0x61B8  # the main thread's slot, the device's queue
+    q0 = lib.mi_cksum_hsa_queues()
     bar = threading.Barrier(16)
-    peak, bad = [], []
+    peak, queues, bad = [], [], []
 
     def work(k):
         for j in range(50):
@@ -210,6 +213,7 @@ def test_dropin_service_slots_are_capped():
             if j == 10:
                 bar.wait(30)
                 peak.append(lib.mi__dropin_service_owners())
+                queues.append(lib.mi_cksum_hsa_queues())
                 bar.wait(30)
 
     try:
@@ -221,9 +225,37 @@ def test_dropin_service_slots_are_capped():
     finally:
         lib.mi__set_dropin_service(was)
     assert not bad, bad[:5]
-    assert 1 <= max(peak) <= 8, peak
-    time.sleep(0.1)
-    assert lib.mi__dropin_service_owners() <= 1  # (the main thread may hold one)
+    assert max(peak) == 17, peak
+    assert set(queues) == {q0}, (queues, q0)
+    deadline = time.monotonic() + 5.0
+    while lib.mi__dropin_service_owners() != 1 and time.monotonic() < deadline:
+        time.sleep(0.01)
+    assert lib.mi__dropin_service_owners() == 1  # the main thread's
+
+
+def test_reused_slot_with_the_same_first_word():
+    """A slot's next owner whose first request would carry exactly the word
+    the previous owner's last one did (same tag, same inline size): the word
+    is changed, the service sees it, the call answers at once."""
+    lib = _lib()
+    was = lib.mi__set_dropin_service(1)
+    res = []
+
+    def work():
+        lib.mi__set_dropin_tag(0x1233)
+        t0 = time.time()
+        res.append((mi.in_cksum_hdr(KAT_HDR, addr_mod=0), time.time() - t0))
+
+    try:
+        for _ in range(3):
+            t = threading.Thread(target=work)
+            t.start()
+            t.join(30)
+            time.sleep(0.05)  # (the thread's key destructor gives its slot back)
+    finally:
+        lib.mi__set_dropin_service(was)
+    assert [v for v, _ in res] == [0x61B8] * 3
+    assert max(dt for _, dt in res) < 2.0, res
 
 
 DEBUG_LIB = os.path.join(LIB_DIR, "debug", "libmicksum.so")

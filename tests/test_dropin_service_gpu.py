@@ -1,10 +1,11 @@
-"""The drop-in service (VERDICT r3 "do this" 6): a resident workgroup per
-calling thread serves the (b1) drop-ins from a mailbox instead of one queue
-dispatch per call.  Its lifetime rules are what these tests exercise: the
-idle exit and the relaunch by the next call (including a request posted just
-as the service leaves), the stop before any other packet of the thread's queue
-(a host burst), the stop before the staging buffer is reallocated, per-thread
-services across thread churn, and the breakdown stamps.  Every result is
+"""The drop-in service (VERDICT r3 "do this" 6; one per device since round 5):
+a resident workgroup serves every thread's (b1) drop-ins and small host
+bursts from its mailbox slot instead of one queue dispatch per call.  Its
+lifetime rules are what these tests exercise: the idle exit and the relaunch
+by the next call (including a request posted just as the service leaves), a
+large host burst dispatched on the same queue while the service runs beside
+it, staging buffer growth (the slot's header follows it), slots across thread
+churn, and the breakdown stamps.  Every result is
 checked against the reference's known answers or the oracle.
 """
 import ctypes as C
@@ -87,10 +88,12 @@ def test_service_idle_exit_and_relaunch(lib):
     assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
 
 
-def test_service_stopped_for_host_burst(lib):
+def test_service_runs_beside_host_burst(lib):
     """A host burst too large for the service (> 64 datagrams) is a dispatch
-    on the same HSA queue: the service is stopped first (else the burst would
-    wait behind it), and the next drop-in starts a new one."""
+    on the device's drop-in queue, not the service's (a packet behind a
+    running kernel on one queue waits for it): it runs beside the resident
+    service and the service stays up.  (The first burst is a warm-up: its
+    first-use costs outlast the service's 1 ms idle exit.)"""
     n, L, stride, first = 200, 1500, 2176, 142
     b = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=3)
     raw = np.zeros(b["buf"].size + 4096, np.uint8)
@@ -102,11 +105,12 @@ def test_service_stopped_for_host_burst(lib):
     want = ORC.ipv4_verify_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
     mi.host_register(raw)
     try:
+        mi.ipv4_verify_host(buf, n, stride=stride, first_off=first, fixed_len=L)
         for k in range(6):
             assert mi.in_cksum_hdr(KAT_HDR, addr_mod=k % 4) == KAT_WANT[k % 4]
             assert lib.mi__dropin_service_live() == 1
             ip, l4, st, bad = mi.ipv4_verify_host(buf, n, stride=stride, first_off=first, fixed_len=L)
-            assert lib.mi__dropin_service_live() == 0
+            assert lib.mi__dropin_service_live() == 1
             assert np.array_equal(st, want[2]) and np.array_equal(l4, want[1])
             assert bad == int((want[2] != 0).sum()) >= 1
     finally:
@@ -114,8 +118,9 @@ def test_service_stopped_for_host_burst(lib):
 
 
 def test_service_staging_growth(lib):
-    """A larger chain than the staging buffer holds: the service is stopped
-    before the buffer is reallocated and restarted on the new one."""
+    """A larger chain than the staging buffer holds: the buffer is
+    reallocated between calls and the slot's header points the service at the
+    new one."""
     sizes = [20, 1500, 65536, 100, 200000, 40, 262144, 64]
     for n in sizes:
         m = mi.MbufChain([(PAT[:n // 2], 1), (PAT[n // 2:n], 2)])
@@ -124,8 +129,8 @@ def test_service_staging_growth(lib):
 
 
 def test_service_thread_churn(lib):
-    """16 threads at a time, each with its own service; after they exit the
-    library's queue count is back and nothing was leaked."""
+    """16 threads at a time, each with a slot of the one service; after they
+    exit the library's queue count is back and nothing was leaked."""
     lib.mi_cksum_hsa_queues.restype = C.c_int
     lib.mi__hsa_queues_leaked.restype = C.c_int
     assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8

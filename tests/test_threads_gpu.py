@@ -2,12 +2,13 @@
 
 The (b1) drop-ins and the host-burst path run on whatever thread calls them
 -- the dpdk_rx kthread, application threads in ud_send, the callout thread
-(SURVEY.md 8(b1) "Threading").  Each calling thread gets its own HSA queue,
-completion signal, kernel-argument slots, staging and streams; a pthread-key
-destructor gives them back when the thread exits.  This test creates and
-joins 64 threads at a time, several rounds, each thread making drop-in calls
-(every eighth a zero-copy host burst through its own AQL queue, every eighth
-a staged one through its own HIP streams), checks every result against the
+(SURVEY.md 8(b1) "Threading").  Each calling thread gets its own completion
+signal, kernel-argument slots, mailbox slot, staging and streams (the HSA
+queue is the device's one drop-in queue, shared); a pthread-key destructor
+gives them back when the thread exits.  This test creates and joins 64
+threads at a time, several rounds, each thread making drop-in calls (every
+eighth a zero-copy host burst through the service or the drop-in queue, every
+eighth a staged one through its own HIP streams), checks every result against the
 reference's known answers / the oracle, and checks that the library's HSA
 queue count is back where it started after every round.  The kernel driver's
 per-process queue list (where readable) must stay flat from the second round
@@ -55,7 +56,7 @@ def _burst(seed):
 def test_thread_churn_keeps_queue_count_flat():
     torch.cuda.init()
     lib = load()
-    # warm the main thread (its queue stays for the process's life)
+    # warm the main thread (the device's drop-in queue stays for the process's life)
     assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
     base = lib.mi_cksum_hsa_queues()
     kfd = []

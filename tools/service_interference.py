@@ -7,8 +7,9 @@ A libuinet process has both at once: the rx kthread's batch offload
 the (b1) drop-ins (ip_output.c:649-672 on the sending threads, here
 in_cksum_hdr on a 20-byte header in a loop).  Each side is measured alone and
 then with the other running, for 1, 4 and 16 drop-in threads, with the
-drop-in service (at most MI_CKSUM_DROPIN_SERVICE_MAX = 8 threads hold one; the
-rest dispatch per call) and with one dispatch per call for every thread:
+drop-in service (one per device since round 5: every thread holds a mailbox
+slot of it) and with one dispatch per call for every thread (on the device's
+one drop-in queue since round 5; a queue per thread before):
 
   batch_gib_s        the batch side's rate (GiB/s of datagram bytes)
   calls_per_s        all drop-in threads together
