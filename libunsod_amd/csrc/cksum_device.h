@@ -206,10 +206,11 @@ __device__ __forceinline__ uint32_t ld_u32(const Arr &a, uint32_t i MI_AT) {
   ARR_CHECK(a, 4u * i, 4u);
   return __builtin_amdgcn_raw_buffer_load_b32(a.r, 4u * i, 0, AUX);
 }
+template <int AUX = 0>
 __device__ __forceinline__ uint64_t ld_u64(const Arr &a, uint32_t i MI_AT) {
   ARR_CHECK(a, 8u * i, 8u);
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(a.r, 8u * i, 0, 0);
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(a.r, 8u * i, 0, AUX);
   return (uint64_t)v.x | ((uint64_t)v.y << 32);
 }
 __device__ __forceinline__ uint32_t ld_u8(const Arr &a, uint32_t i MI_AT) {
@@ -263,17 +264,22 @@ __device__ __forceinline__ Arr offs_arr(const Desc &d) {
   return arr_of(d.offs, (uint64_t)d.n * ((d.flags & MI_BATCH_OFFS32) ? 4u : 8u));
 }
 __device__ __forceinline__ Arr lens_arr(const Desc &d) { return arr_of(d.lens, (uint64_t)d.n * 4u); }
+// (AUX: the descriptor loads' cache policy -- kSys for descriptors the host
+// rewrites under a resident kernel, svc_burst)
+template <int AUX = 0>
 __device__ __forceinline__ uint64_t desc_off(const Desc &d, uint32_t i) {
   if (!d.offs) return d.first_off + (uint64_t)i * d.stride;
   const Arr a = offs_arr(d);
-  return (d.flags & MI_BATCH_OFFS32) ? (uint64_t)ld_u32(a, i) : ld_u64(a, i);
+  return (d.flags & MI_BATCH_OFFS32) ? (uint64_t)ld_u32<AUX>(a, i) : ld_u64<AUX>(a, i);
 }
+template <int AUX = 0>
 __device__ __forceinline__ uint32_t pkt_off(const Desc &d, uint32_t i) {
-  const uint64_t o = desc_off(d, i);
+  const uint64_t o = desc_off<AUX>(d, i);
   return o < kOOB ? (uint32_t)o : kOOB;
 }
+template <int AUX = 0>
 __device__ __forceinline__ uint32_t pkt_len(const Desc &d, uint32_t i) {
-  const uint32_t l = d.lens ? ld_u32(lens_arr(d), i) : d.fixed_len;
+  const uint32_t l = d.lens ? ld_u32<AUX>(lens_arr(d), i) : d.fixed_len;
   return l < 0x7fff0000u ? l : 0x7fff0000u;
 }
 // Packet bytes are read once: nontemporal loads (aux = 2, `nt`) measured +10 %
@@ -432,7 +438,10 @@ __device__ __forceinline__ void fold_pass(const u32x4 (&v)[U], uint32_t p, int l
 // A 20-byte header -- the common case -- is summed from the five dwords the
 // header parse already holds; only datagrams with IP options (hl > 20) fold
 // their header from the chunks.
-template <int G, int U, bool TX>
+// COH: every load of the datagram's bytes system-coherent (kSys) instead of
+// nontemporal -- bytes the host rewrites under a resident kernel (svc_burst),
+// read with no acquire fence.
+template <int G, int U, bool TX, bool COH = false>
 __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t flen,
                                           int lane, u32x4 (&v)[U], IpHdr &ih, bool &hdr_ok,
                                           bool &l4_ok, uint32_t &sum_h, uint32_t &sum_l,
@@ -456,7 +465,7 @@ __device__ __forceinline__ void ipv4_sums(__amdgpu_buffer_rsrc_t r, uint32_t off
   for (uint32_t p = 0;;) {
     fold_pass<G, U, TX>(v, p, lane, h, lend, hend, opts, acc_t, acc_h, acc_f);
     if (++p >= npass) break;
-    issue_pass<G, U>(r, c0, nch, p, lane, v);
+    issue_pass<G, U, COH ? kSys : 2>(r, c0, nch, p, lane, v);
   }
   const uint32_t total = group_sum<G>(acc_t);
   uint32_t hdr, field;
@@ -573,6 +582,7 @@ __device__ __forceinline__ void for_each_packet(const Desc &d, __amdgpu_buffer_r
 //    bytes, udp_usrreq.c:406-414); never for fragments (ip_reass sums csum_data of the
 //    pieces, no pseudo header) or other protocols.
 // Malformed headers get no flags: the stack's own length checks drop them.
+template <bool COH = false>
 __device__ __forceinline__ void rx_offload_flags(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
                                                  bool hdr_ok, bool l4_ok, uint32_t ip, uint32_t l4, uint32_t &fl,
                                                  uint32_t &cd) {
@@ -585,8 +595,8 @@ __device__ __forceinline__ void rx_offload_flags(__amdgpu_buffer_rsrc_t r, uint3
     bool l4v = l4_ok && (ip_off & 0x3fffu) == 0u;  // IP_MF | IP_OFFMASK
     if (l4v && ih.proto == 17u) {
       const uint32_t u = off + ih.hl + 4u;  // uh_ulen, big-endian
-      const uint32_t ulen = plen >= 8u ? ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, u, 0, 0) << 8) |
-                                             __builtin_amdgcn_raw_buffer_load_b8(r, u + 1u, 0, 0)
+      const uint32_t ulen = plen >= 8u ? ((uint32_t)__builtin_amdgcn_raw_buffer_load_b8(r, u, 0, COH ? kSys : 0) << 8) |
+                                             __builtin_amdgcn_raw_buffer_load_b8(r, u + 1u, 0, COH ? kSys : 0)
                                        : ~0u;
       l4v = ulen == plen;
     } else {
@@ -604,30 +614,35 @@ __device__ __forceinline__ void rx_offload_flags(__amdgpu_buffer_rsrc_t r, uint3
 // bytes it re-reads were just streamed, so they come from L2.
 
 // Absolute-lane sum of bytes [a, b) of the datagram at off.
+template <bool COH = false>
 __device__ __forceinline__ uint32_t dgram_range(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t a,
                                                 uint32_t b) {
   uint32_t s = 0;
   for (uint32_t c = (off + a) & ~15u; c < off + b; c += 16u)
-    s += range_sum(__builtin_amdgcn_raw_buffer_load_b128(r, c, 0, 0), (int)(c - off), (int)a, (int)b);
+    s += range_sum(__builtin_amdgcn_raw_buffer_load_b128(r, c, 0, COH ? kSys : 0), (int)(c - off), (int)a, (int)b);
   return s;
 }
+template <bool COH = false>
 __device__ __forceinline__ uint32_t ld_byte(__amdgpu_buffer_rsrc_t r, uint32_t o) {
-  return __builtin_amdgcn_raw_buffer_load_b8(r, o, 0, 0);
+  return __builtin_amdgcn_raw_buffer_load_b8(r, o, 0, COH ? kSys : 0);
 }
+template <bool COH = false>
 __device__ __forceinline__ uint32_t ld_be16(__amdgpu_buffer_rsrc_t r, uint32_t o) {
-  return (ld_byte(r, o) << 8) | ld_byte(r, o + 1u);
+  return (ld_byte<COH>(r, o) << 8) | ld_byte<COH>(r, o + 1u);
 }
 // Absolute-lane sum of the span [hl, hl + span) given S = sum of [hl, ip_len):
 // whichever of the span or the rest is shorter is re-read (S is exact, < 2^31).
+template <bool COH = false>
 __device__ __forceinline__ uint32_t l4_span_sum(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
                                                 uint32_t span, uint32_t S) {
   const uint32_t plen = ih.iplen - ih.hl;
   if (span >= plen) return S;
-  if (span <= plen - span) return dgram_range(r, off, ih.hl, ih.hl + span);
-  return S - dgram_range(r, off, ih.hl + span, ih.iplen);
+  if (span <= plen - span) return dgram_range<COH>(r, off, ih.hl, ih.hl + span);
+  return S - dgram_range<COH>(r, off, ih.hl + span, ih.iplen);
 }
 
 // RX: the L4 value the protocol input routine tests (mi_cksum.h, MI_BATCH_DEMUX).
+template <bool COH = false>
 __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off, const IpHdr &ih,
                                          bool odd, uint32_t sum_l, uint32_t &l4, uint32_t &st) {
   const uint32_t plen = ih.iplen - ih.hl;
@@ -654,7 +669,7 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
     return;
   }
   if (ih.proto == 17u) {
-    const uint32_t ulen = ld_be16(r, off + ih.hl + 4u);  // udp_usrreq.c:406-414
+    const uint32_t ulen = ld_be16<COH>(r, off + ih.hl + 4u);  // udp_usrreq.c:406-414
     if (ulen != plen) {
       if (ulen > plen || ulen < 8u) {
         st |= MI_ST_MALFORMED;
@@ -662,12 +677,12 @@ __device__ __forceinline__ void demux_l4(__amdgpu_buffer_rsrc_t r, uint32_t off,
       }
       span = ulen;  // m_adj to uh_ulen
     }
-    if (ld_be16(r, off + ih.hl + 6u) == 0u) {  // uh_sum == 0: udps_nosum
+    if (ld_be16<COH>(r, off + ih.hl + 6u) == 0u) {  // uh_sum == 0: udps_nosum
       st |= MI_ST_L4_NONE;
       return;
     }
   }
-  uint32_t sl = fold16(l4_span_sum(r, off, ih, span, sum_l));
+  uint32_t sl = fold16(l4_span_sum<COH>(r, off, ih, span, sum_l));
   if (odd) sl = swap16(sl);
   if (pseudo) {
     const uint64_t seed = (uint64_t)ih.src + ih.dst + (ih.proto << 8) + swap16(span);
@@ -704,6 +719,7 @@ struct VOut {
   uint32_t i = ~0u;  // ~0u: nothing pending
   uint32_t ip = 0, l4 = 0, st = 0, fl = 0, cd = 0;
 };
+template <bool COH = false>
 __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr &ih, bool hdr_ok, bool l4_ok,
                                               uint32_t sum_h, uint32_t sum_l, const Desc &d,
                                               __amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -719,7 +735,7 @@ __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr 
     if (!l4_ok) {
       st = MI_ST_MALFORMED;
     } else if (d.flags & MI_BATCH_DEMUX) {
-      demux_l4(r, off, ih, odd, sum_l, l4, st);
+      demux_l4<COH>(r, off, ih, odd, sum_l, l4, st);
     } else {
       uint32_t sl = fold16(sum_l);
       if (odd) sl = swap16(sl);
@@ -732,7 +748,7 @@ __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr 
   o.ip = ip;
   o.l4 = l4;
   o.st = st;
-  if (d.cflags) rx_offload_flags(r, off, ih, hdr_ok, l4_ok, ip, l4, o.fl, o.cd);
+  if (d.cflags) rx_offload_flags<COH>(r, off, ih, hdr_ok, l4_ok, ip, l4, o.fl, o.cd);
   return o;
 }
 
@@ -740,18 +756,21 @@ __device__ __forceinline__ VOut verify_result(uint32_t i, bool odd, const IpHdr 
 // counter), so a datagram index can only ever land inside its own array.
 // (Plain global stores and buffer stores of the default policy measured the
 // same, profiles/r03/serial_floor_r03.jsonl.)
+// (COH: system-coherent stores -- write-through, so a wait for their acks
+// orders them before a result word with no release fence, svc_burst)
+template <bool COH = false>
 __device__ __forceinline__ void verify_emit(const VOut &o, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const Desc &d) {
   if (o.i == ~0u) return;
-  constexpr int kOA = MI_OUT_AUX >= 0 ? MI_OUT_AUX : 0;
+  constexpr int kOA = COH ? kSys : MI_OUT_AUX >= 0 ? MI_OUT_AUX : 0;
   const uint64_t n = d.n;
   if (ip_out) st_u16<kOA>(arr_of(ip_out, 2u * n), o.i, o.ip);
   if (l4_out) st_u16<kOA>(arr_of(l4_out, 2u * n), o.i, o.l4);
   if (st_out) st_u8<kOA>(arr_of(st_out, n), o.i, o.st);
   if (bad && (o.st & ~MI_ST_L4_NONE)) add_u32(arr_of(bad, 4u), 0u, 1u);
   if (d.cflags) {
-    st_u32(arr_of(d.cflags, 4u * n), o.i, o.fl);
-    if (d.cdata) st_u32(arr_of(d.cdata, 4u * n), o.i, o.cd);
+    st_u32<COH ? kSys : 0>(arr_of(d.cflags, 4u * n), o.i, o.fl);
+    if (d.cdata) st_u32<COH ? kSys : 0>(arr_of(d.cdata, 4u * n), o.i, o.cd);
   }
 }
 

@@ -1563,23 +1563,29 @@ constexpr uint32_t kSvcBurstMax = 128;  // datagrams (descriptors inline: 128 + 
 #define MI_SVC_BURST_G 8  // lanes per datagram in a service burst: 64 datagrams per round (16: 32)
 #endif
 // The burst, one lane group per datagram (verify_body's per-datagram work:
-// ip_input.c:459-471 + tcp_input.c:697-720 / the RX offload flags).
+// ip_input.c:459-471 + tcp_input.c:697-720 / the RX offload flags).  Every
+// load -- descriptors in the slot, datagram bytes in host memory -- is
+// system-coherent (kSys), and so is every output store: the service needs no
+// acquire fence before a burst (an L2 invalidate per request, under the batch
+// kernels sharing the L2) and no release after it, only a wait for the
+// stores' acknowledgements (profiles/r05/burst_breakdown_*.jsonl).
 __device__ __forceinline__ void svc_burst(const BurstArgs &a) {
   constexpr int G = MI_SVC_BURST_G, U = 1536 / (16 * MI_SVC_BURST_G);  // 1536 bytes per pass
   const Desc &d = a.d;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const int lane = threadIdx.x & (G - 1);
   for (uint32_t i = threadIdx.x / G; i < d.n; i += kScalarThreads / G) {
-    const uint32_t off = pkt_off(d, i), flen = pkt_len(d, i);
+    const uint32_t off = pkt_off<kSys>(d, i), flen = pkt_len<kSys>(d, i);
     u32x4 v[U];
-    issue_first<G, U>(r, off, flen, lane, v);
+    issue_first<G, U, kSys>(r, off, flen, lane, v);
     IpHdr ih;
     bool hdr_ok, l4_ok;
     uint32_t sum_h, sum_l;
-    ipv4_sums<G, U, false>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
+    ipv4_sums<G, U, false, true>(r, off, flen, lane, v, ih, hdr_ok, l4_ok, sum_h, sum_l);
     if (lane == 0)
-      verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off), a.ip,
-                  a.l4, a.st, a.bad, d);
+      verify_emit<true>(
+          verify_result<true>(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off), a.ip,
+          a.l4, a.st, a.bad, d);
   }
 }
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint32_t *slab, uint32_t nslots,
@@ -1686,15 +1692,16 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
     const uint32_t sq = req[0], s = req[1];
     uint32_t *const out = (uint32_t *)s_ptr[0];
     if (req[11]) {
-      // a host RX burst: every wave, then the result word once every wave's
-      // outputs are visible at system scope.  field 2: diagnostics only
-      // (MI_CKSUM_BURST_FENCES, tools/burst_breakdown.py): bit 0 drops the
-      // acquire, bit 1 replaces the release by a wait for the stores' acks;
-      // field 10 (trace): out[1], out[6], out[7] get the clock after the
-      // acquire, after the burst and after the release, from the request seen
+      // a host RX burst: every wave (system-coherent loads and stores,
+      // svc_burst), then the result word once every wave's stores are
+      // acknowledged.  field 2: diagnostics only (MI_CKSUM_BURST_FENCES,
+      // tools/burst_breakdown.py): bit 0 adds a system-scope acquire before
+      // the burst, bit 1 a release after it; field 10 (trace): out[1], out[6],
+      // out[7] get the clock after the acquire, after the burst and after the
+      // release, from the moment the request was seen
       const uint32_t mode = req[2];
       const bool trace = req[10] != 0u;
-      if (!(mode & 1u)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (mode & 1u) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       const uint64_t ta = rt_clock();
       // the arguments, wave-uniform (they build the burst's resources)
       uint32_t w[sizeof(BurstArgs) / 4];
@@ -1709,7 +1716,7 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
         __syncthreads();
         tb = rt_clock();
       }
-      if (!(mode & 2u))
+      if (mode & 2u)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       else
         __builtin_amdgcn_s_waitcnt(0);
@@ -3330,33 +3337,39 @@ int slab_alloc(AqlDevice *a) {
   return 0;
 }
 
-// The device's drop-in queue, the service's completion signal, argument block
-// and exit word, and the slab (created once, on first use).
+// The service's completion signal, argument block and exit word, and the slab
+// (created once, on first use).  The two queues come later, each on its first
+// packet (dq_queue_locked): a queue costs the batch path nothing while it has
+// never held work, so a process that only uses the service never has a
+// dispatch queue, and one that only dispatches never has a service queue.
 int dq_open(AqlDevice *a) {
   std::lock_guard<std::mutex> lk(a->dq_mu);
-  if (a->dq) return 0;
-  if (a->dq_rc) return set_err(a->dq_rc, "AQL engine: the drop-in queue could not be set up");
-  hsa_queue_t *q = nullptr, *sq = nullptr;
-  int rc = aql_queue_create(a->agent, 256, &a->dq_err, &q);
-  if (!rc) rc = aql_queue_create(a->agent, 64, &a->dq_err, &sq);
-  if (!rc && hsa_signal_create(0, 0, nullptr, &a->svc_sig) != HSA_STATUS_SUCCESS)
+  if (a->svc_host) return 0;
+  if (a->dq_rc) return set_err(a->dq_rc, "AQL engine: the drop-in state could not be set up");
+  int rc = 0;
+  if (hsa_signal_create(0, 0, nullptr, &a->svc_sig) != HSA_STATUS_SUCCESS)
     rc = set_err(-EIO, "AQL engine: hsa_signal_create failed");
   if (!rc && jhostmalloc((void **)&a->svc_karg, 512, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
     rc = set_err(-ENOMEM, "drop-in service: kernel-argument block");
-  if (!rc && (jhostmalloc((void **)&a->svc_host, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-              hipHostGetDevicePointer((void **)&a->svc_host_dev, (void *)a->svc_host, 0) != hipSuccess))
+  uint32_t *h = nullptr;
+  if (!rc && (jhostmalloc((void **)&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+              hipHostGetDevicePointer((void **)&a->svc_host_dev, (void *)h, 0) != hipSuccess))
     rc = set_err(-ENOMEM, "drop-in service: exit word");
   if (!rc) rc = slab_alloc(a);
   if (rc) {
     a->dq_rc = rc;
-    aql_queue_destroy(q);
-    aql_queue_destroy(sq);
     return rc;
   }
-  a->svc_host[0] = 0;
-  a->sq = sq;
-  a->dq = q;
+  h[0] = 0;
+  a->svc_host = h;
   return 0;
+}
+// The dispatch queue (svc false) or the service's queue, created on first use
+// (under dq_mu); nullptr with the error set if it cannot be.
+hsa_queue_t *dq_queue_locked(AqlDevice *a, bool svc) {
+  hsa_queue_t *&q = svc ? a->sq : a->dq;
+  if (!q && aql_queue_create(a->agent, svc ? 64u : 256u, &a->dq_err, &q)) q = nullptr;
+  return q;
 }
 
 // One dispatch packet into the device's drop-in queue.  The kernel arguments
@@ -3413,7 +3426,7 @@ void svc_stop_locked(AqlDevice *a, double timeout_s) {
 }
 void svc_atexit() {
   for (AqlDevice &a : g_aql) {
-    if (!a.dq) continue;
+    if (!a.svc_host) continue;
     std::unique_lock<std::mutex> lk(a.dq_mu, std::try_to_lock);  // (a thread mid-call may hold it)
     svc_stop_locked(&a, 0.2);
   }
@@ -3467,7 +3480,8 @@ int svc_ensure(AqlDevice *a) {
   const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
   const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8), a->svc_host_dev, token, dropin_svc_idle_ticks()};
   hsa_signal_store_relaxed(a->svc_sig, 1);
-  int rc = dq_dispatch_locked(a, a->sq, kAqlSvc, 1, kScalarThreads, &s, sizeof s, a->svc_karg, a->svc_sig);
+  hsa_queue_t *q = dq_queue_locked(a, true);
+  int rc = q ? dq_dispatch_locked(a, q, kAqlSvc, 1, kScalarThreads, &s, sizeof s, a->svc_karg, a->svc_sig) : -EIO;
   if (rc) {
     hsa_signal_store_relaxed(a->svc_sig, 0);
     return rc;
@@ -3588,7 +3602,8 @@ int aql_one_submit(int id, unsigned blocks, unsigned wg, const void *args, uint3
   if (wait) hsa_signal_store_relaxed(o.sig, 1);
   {
     std::lock_guard<std::mutex> lk(o.dev->dq_mu);
-    rc = dq_dispatch_locked(o.dev, o.dev->dq, id, blocks, wg, args, nargs, ka, wait ? o.sig : hsa_signal_t{0});
+    hsa_queue_t *q = dq_queue_locked(o.dev, false);
+    rc = q ? dq_dispatch_locked(o.dev, q, id, blocks, wg, args, nargs, ka, wait ? o.sig : hsa_signal_t{0}) : -EIO;
   }
   if (rc) return rc;
   if (t_dtrace.on) t_dtrace.t_doorbell = sys_ts();
@@ -5178,7 +5193,7 @@ int mi__set_dropin_service(int on) {
   const int was = dropin_svc_on() ? 1 : 0;
   g_dropin_svc.store(on ? 1 : 0);
   AqlDevice *a = t_aql1.dev;
-  if (!on && a && a->dq) {
+  if (!on && a && a->svc_host) {
     std::lock_guard<std::mutex> lk(a->dq_mu);
     svc_stop_locked(a, 1.0);
   }
@@ -5207,8 +5222,28 @@ int mi__spin(uint32_t us, int via) {
   if ((rc = aql_one_open(o))) return rc;
   uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
   std::lock_guard<std::mutex> lk(o.dev->dq_mu);
-  return dq_dispatch_locked(o.dev, via == 1 ? o.dev->sq : o.dev->dq, kAqlSpin, 1, 64, &ticks, sizeof ticks, ka,
-                            hsa_signal_t{0});
+  hsa_queue_t *q = dq_queue_locked(o.dev, via == 1);
+  return q ? dq_dispatch_locked(o.dev, q, kAqlSpin, 1, 64, &ticks, sizeof ticks, ka, hsa_signal_t{0}) : -EIO;
+}
+// Diagnostics (tools/queue_place_probe.py): a resident wave for `us`
+// microseconds on the k-th of up to 16 extra queues of the calling thread's
+// device (created in order on first use, 64 packets; prio >= 0: set the
+// queue's priority first, 0 low .. 2 high).
+int mi__spin_queue(uint32_t us, int k, int prio) {
+  static hsa_queue_t *qs[16];
+  static std::atomic<int> qerr{0};
+  if (k < 0 || k >= 16) return set_err(-EINVAL, "queue index");
+  int rc = ensure_ctx();
+  AqlOne &o = t_aql1;
+  if (rc || (rc = aql_one_open(o))) return rc;
+  std::lock_guard<std::mutex> lk(o.dev->dq_mu);
+  for (int j = 0; j <= k; ++j)
+    if (!qs[j] && (rc = aql_queue_create(o.dev->agent, 64, &qerr, &qs[j]))) return rc;
+  if (prio >= 0 && hsa_amd_queue_set_priority(qs[k], (hsa_amd_queue_priority_t)prio) != HSA_STATUS_SUCCESS)
+    return set_err(-EIO, "hsa_amd_queue_set_priority");
+  const uint64_t ticks = (uint64_t)us * 100u;
+  uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
+  return dq_dispatch_locked(o.dev, qs[k], kAqlSpin, 1, 64, &ticks, sizeof ticks, ka, hsa_signal_t{0});
 }
 // Is the drop-in service of the calling thread's device running?  (tests)
 int mi__dropin_service_live(void) {

@@ -8,9 +8,12 @@ posted (host clock, from entry), and on the GPU's 100 MHz clock from the
 moment the service saw the request: acquire done, burst verified (all waves),
 release done, result stored; then the result seen by the host.  Medians of
 --iters calls per n and per fence mode (MI_CKSUM_BURST_FENCES is read once per
-process, so each mode runs in a child process: 0 = acquire + release, the
-product; 1 = no acquire; 2 = stores' acks instead of the release; 3 = both --
-1-3 are diagnostics: correct only for uncached host memory).
+process, so each mode runs in a child process): round 5's product, 0, reads
+and writes system-coherent with no fences (a wait for the stores' acks before
+the result word); 1 adds a system-scope acquire before the burst, 2 a release
+after it, 3 both (round 4's fences, now redundant).  profiles/r05/
+burst_breakdown_r05a.jsonl is the earlier build (default-policy loads and
+stores: 0 = both fences, 1 = no acquire).
 
     python tools/burst_breakdown.py [--sizes 1,8,32,64] [--modes 0,1,2,3]
 """
