@@ -4411,18 +4411,24 @@ int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
 // Ranges registered through mi_cksum_host_register: the zero-copy path reads
 // a host batch in place only when every byte its loads can touch lies inside
 // one of them (a read past a mapping would fault the GPU).
+// Each keeps the GPU address of its registered pointer, found once at
+// registration, instead of a hipHostGetDevicePointer (a runtime lookup) per
+// call.
 struct HostRange {
-  uintptr_t lo, hi;
+  uintptr_t lo, hi;  // whole pages
+  uintptr_t p, dev;  // the registered pointer and its GPU address
 };
 static std::mutex g_reg_mu;
 static std::vector<HostRange> g_reg;
 
-static bool host_range_mapped(const void *p, uint64_t bytes) {
+// The GPU address of host bytes [p, p + bytes) (rounded up to 16), or nullptr
+// when they do not lie inside one registered range.
+static void *host_dev_ptr(const void *p, uint64_t bytes) {
   const uintptr_t lo = (uintptr_t)p, hi = lo + ((bytes + 15u) & ~15ull);
   std::lock_guard<std::mutex> g(g_reg_mu);
   for (const HostRange &r : g_reg)
-    if (lo >= r.lo && hi <= r.hi) return true;
-  return false;
+    if (lo >= r.lo && hi <= r.hi) return (void *)(r.dev + (lo - r.p));
+  return nullptr;
 }
 
 int mi_cksum_host_register(void *p, uint64_t bytes) {
@@ -4431,10 +4437,15 @@ int mi_cksum_host_register(void *p, uint64_t bytes) {
   HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
   jnote("host register", p, bytes);
   dbg_mem("host-register", p, bytes);
+  void *dev = nullptr;
+  if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
+    (void)hipHostUnregister(p);
+    return set_err(-EIO, "mi_cksum_host_register: no device address for the range");
+  }
   // the mapping covers whole pages
   const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + bytes + 4095) & ~(uintptr_t)4095;
   std::lock_guard<std::mutex> g(g_reg_mu);
-  g_reg.push_back({lo, hi});
+  g_reg.push_back({lo, hi, (uintptr_t)p, (uintptr_t)dev});
   return 0;
 }
 
@@ -4733,12 +4744,8 @@ static int host_batch(const mi_pkt_batch *b, const HostOut &o, uint32_t *bad_cou
     return !(e && e[0] == '0');
   }();
   if (allow_zc && !(b->flags & MI_BATCH_HOST_STAGED) && b->bytes && b->bytes <= kMaxBytes &&
-      ((uintptr_t)b->base & 15u) == 0 &&
-      host_range_mapped(b->base, b->bytes)) {
-    void *dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, b->base, 0) == hipSuccess && dp)
-      return verify_host_zero_copy(b, (const uint8_t *)dp, o, bad_count);
-    (void)hipGetLastError();  // not registered: staged path
+      ((uintptr_t)b->base & 15u) == 0) {
+    if (void *dp = host_dev_ptr(b->base, b->bytes)) return verify_host_zero_copy(b, (const uint8_t *)dp, o, bad_count);
   }
   static const uint64_t kChunk = [] {
     const char *s = getenv("MI_CKSUM_HOST_CHUNK");
@@ -4937,11 +4944,9 @@ int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags)
   const Shape sh = pick_tx_shape(b->max_len ? b->max_len : b->room);
   void *sdev = nullptr, *ddev = nullptr;
   const bool zc = !(flags & MI_TX_HOST_STAGED) && b->src && b->dst && b->src_bytes && b->dst_bytes &&
-                  b->src_bytes <= kMaxBytes && b->dst_bytes <= kMaxBytes && host_range_mapped(b->src, b->src_bytes) &&
-                  host_range_mapped(b->dst, b->dst_bytes) &&
-                  hipHostGetDevicePointer(&sdev, const_cast<void *>(b->src), 0) == hipSuccess &&
-                  hipHostGetDevicePointer(&ddev, b->dst, 0) == hipSuccess && sdev && ddev;
-  (void)hipGetLastError();
+                  b->src_bytes <= kMaxBytes && b->dst_bytes <= kMaxBytes &&
+                  (sdev = host_dev_ptr(b->src, b->src_bytes)) != nullptr &&
+                  (ddev = host_dev_ptr(b->dst, b->dst_bytes)) != nullptr;
   if (zc) {
     // zero-copy: descriptors and status through the mapped per-thread block
     if (c.zhost_cap < need) {
