@@ -594,6 +594,9 @@ def dropin_latency(mi, calls: int = 400) -> dict:
             ts.append(time.perf_counter() - t0)
         return round(float(np.median(ts)) * 1e6, 3)
 
+    # (the library keeps the drop-in service out of the way for 0.5 ms after
+    # a batch submission -- DESIGN.md 5.6 -- so these start well after one)
+    time.sleep(0.01)
     out = dict(unit="us per call (median)", calls=calls,
                ctypes_floor_us=med(lib.in_addword, (1, 2)))
     ref = None

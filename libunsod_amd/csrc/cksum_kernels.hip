@@ -348,9 +348,13 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 // NW: waves per workgroup (each wave owns its own 64-datagram ranges and LDS
 // rows; a smaller workgroup frees its LDS as soon as its own waves are done,
 // not when the slowest of four heavy-tailed ranges is).
-template <int U, int MODE = 0, int NW = kBlock / 64>
+// RG (byte-balanced ranges, VERDICT r4 "do this" 3, experiment): wave w
+// takes datagrams [starts[w], starts[w+1]) -- at most 64, cut so each range
+// holds about the same bytes -- instead of the 64 at 64 w; one range per wave.
+template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
-                                            uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes) {
+                                            uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes,
+                                            const uint32_t *starts = nullptr, uint32_t nr = 0) {
   constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[NW][W];
@@ -359,14 +363,24 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
 #endif
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t rstride = gridDim.x * NW * 64u;
+  uint32_t rstride = gridDim.x * NW * 64u;
   uint32_t *sq = s_q[wv];
-  uint32_t p0 = (blockIdx.x * NW + wv) * 64u;
+  uint32_t p0 = (blockIdx.x * NW + wv) * 64u, cnt = 64u;
+  if constexpr (RG) {
+    const uint32_t w = blockIdx.x * NW + wv;
+    if (w >= nr) return;
+    const Arr sa = arr_of(starts, 4ull * (nr + 1u));
+    const uint32_t b = lane < 2u ? ld_u32(sa, w + lane) : 0u;
+    p0 = (uint32_t)__builtin_amdgcn_readlane((int)b, 0);
+    const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)b, 1);
+    cnt = p1 > p0 ? min(p1 - p0, 64u) : 0u;
+    rstride = d.n;  // one range per wave: the loop ends after it
+  }
   if (p0 >= d.n) return;
   // descriptors of this lane's datagram; the next range's are fetched while
   // this range is folded
-  uint32_t off = p0 + lane < d.n ? pkt_off(d, p0 + lane) : 0u;
-  uint32_t flen = p0 + lane < d.n ? pkt_len(d, p0 + lane) : 0u;
+  uint32_t off = p0 + lane < d.n && lane < cnt ? pkt_off(d, p0 + lane) : 0u;
+  uint32_t flen = p0 + lane < d.n && lane < cnt ? pkt_len(d, p0 + lane) : 0u;
   // this lane's previous datagram's stores, issued once the next range's first
   // pass is in flight (VOut: vmcnt counts stores with loads)
   VOut pend;
@@ -374,7 +388,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
   uint32_t ptx_off = 0;
   for (;;) {
     const uint32_t i = p0 + lane;
-    const bool act = i < d.n;
+    const bool act = i < d.n && lane < cnt;
     const uint32_t end = act ? off + flen : 0u;
     // (a span's sum must stay below 2^32 for Q(end) - Q(start) to be exact)
     const bool sane = !act || (off < kOOB && end >= off && end <= d.bytes && (!SPAN || flen <= 65535u));
@@ -552,6 +566,12 @@ __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Des
                                                                 uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
                                                                 uint32_t abs_lanes) {
   packed_body<U, MODE, NW>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+}
+template <int U, int NW>
+__global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_ranges(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                                uint8_t *st_out, uint32_t *bad, const uint32_t *starts,
+                                                                uint32_t nr) {
+  packed_body<U, 0, NW, true>(d, ip_out, l4_out, st_out, bad, SpanSeeds{}, 0u, starts, nr);
 }
 
 // The bounds of a wave's 64-datagram range (the flat-run kernels): the run
@@ -2136,6 +2156,7 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
 
 // The journal entries of a launch over a batch (fault reporter): the launch,
 // then the arrays it references with their extents.
+void batch_activity(int device);  // (the drop-in service stands aside)
 void jdesc(const char *what, uint32_t tag, const Desc &d, const void *ip = nullptr, const void *l4 = nullptr,
            const void *st = nullptr, const void *bad = nullptr) {
   jnote(what, nullptr, 0, tag);
@@ -2384,6 +2405,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
   unsigned dblocks = 0;
   if (deal && pl.kind == kPlanShape && deal_plan(d, pl.shape, deal_kernel, &dfn, &dblocks)) {
     jdesc("launch verify (dealt units)", (uint32_t)(pl.shape.g * 100 + pl.shape.u), d, ip, l4, st, bad);
+    batch_activity(t_ctx.device);
     jnote("  deal counters", deal, kDealSetBytes, dblocks);
 #define X(G_, U_)                                                                                              \
   if (pl.shape.g == G_ && pl.shape.u == U_) {                                                                  \
@@ -2395,6 +2417,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
   }
   jdesc("launch verify", (uint32_t)pl.kind * 1000u + (pl.dma ? 100u + pl.dma : pl.run_u * 10u + pl.run_nw), d, ip, l4, st,
         bad);
+  batch_activity(t_ctx.device);
   if (pl.kind == kPlanRun && pl.dma) {
 #define X(U_, R_)                                                                                            \
   if (pl.dma == 10 * U_ + R_) {                                                                              \
@@ -2444,6 +2467,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
 int launch_span(const Desc &d, Shape sh, uint32_t abs_lanes, const SpanSeeds &sd, uint16_t *out,
                 hipStream_t s) {
   jdesc("launch span", (uint32_t)(sh.g * 100 + sh.u), d, out);
+  batch_activity(t_ctx.device);
   if (sd.seeds) jnote("  seeds", sd.seeds, 4ull * d.n);
   if (sd.src) jnote("  src/dst/proto", sd.src, 4ull * d.n);
   if (sd.plens) jnote("  plens", sd.plens, 4ull * d.n);
@@ -2492,6 +2516,7 @@ bool finalize_uses_vlaunch(const Desc &) { return true; }  // every finalize pla
 
 int launch_finalize(const Desc &d, Shape sh, hipStream_t s, uint32_t max_len) {
   jdesc("launch finalize", (uint32_t)(sh.g * 100 + sh.u), d);
+  batch_activity(t_ctx.device);
   // packed mixed lengths and dense slots: the flat-run kernel (as verify_plan
   // picks it for verify), one lane group per datagram otherwise
   const bool dense_slots = !d.offs && !d.lens && d.stride && d.stride <= ((d.fixed_len + 63u) & ~63u) + 64u;
@@ -2550,6 +2575,7 @@ int tx_kernel_kind() {
 }
 
 int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
+  batch_activity(t_ctx.device);
   jnote("launch tx_copy", nullptr, 0, (uint32_t)(sh.g * 100 + sh.u));
   jnote("  src", t.src, t.src_bytes, t.n);
   jnote("  dst", t.dst, t.dst_bytes);
@@ -3135,6 +3161,7 @@ int aql_wait(AqlRun *a) {
 
 // Submit `steps` passes starting with batch j0.
 int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
+  batch_activity(t_ctx.device);
   if (!steps) return 0;
   jnote("launch aql run", a->kargs, a->kargs_bytes, steps);
   const uint32_t nb = (uint32_t)(a->pkt.size() / a->nq);
@@ -3424,6 +3451,55 @@ void svc_stop_locked(AqlDevice *a, double timeout_s) {
   if (a->svc_host[0] != a->svc_token)
     fprintf(stderr, "libmicksum: the drop-in service did not stop within %.0f ms\n", timeout_s * 1e3);
 }
+// Batch activity.  A resident drop-in service whose queue shares a hardware
+// pipe with a busy batch queue costs that queue its overlap with the other
+// (0.65x of the 1500 B batch rate), a service on another pipe costs nothing,
+// and the HSA API does not say which pipe a queue gets (DESIGN.md 5.6,
+// profiles/r05/queue_place_probe_r05.jsonl).  So the service stands aside
+// while the library's own batch path is busy: every batch submission (a
+// launch, a prepared run) notes the time and, if the device's service is
+// running, moves its control word (no wait: it leaves at its next idle poll,
+// and no new requests come -- a drop-in or small burst within the quiet time
+// of the latest submission dispatches instead, which leaves the batch
+// 0.90-0.96 of its rate); a service relaunched in that time (for a request
+// posted as it left) gets a short idle exit.  MI_CKSUM_SERVICE_QUIET_US
+// (default 500; 0: never stand aside).
+int64_t now_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+}
+std::atomic<int64_t> g_batch_ns{INT64_MIN / 2};
+int64_t batch_quiet_ns() {
+  static const int64_t q = [] {
+    const char *e = getenv("MI_CKSUM_SERVICE_QUIET_US");
+    const long v = e ? atol(e) : 500L;
+    return (int64_t)(v > 0 ? v : 0) * 1000;
+  }();
+  return q;
+}
+bool batch_busy() {
+  const int64_t q = batch_quiet_ns();
+  return q && now_ns() - g_batch_ns.load(std::memory_order_relaxed) < q;
+}
+thread_local bool t_host_path = false;  // inside a host-memory batch call: not the batch path (PCIe-bound latency work)
+struct HostPath {
+  HostPath() { t_host_path = true; }
+  ~HostPath() { t_host_path = false; }
+};
+void batch_activity(int device) {
+  if (!batch_quiet_ns() || t_host_path) return;
+  g_batch_ns.store(now_ns(), std::memory_order_relaxed);
+  if (device < 0 || device >= 64) return;
+  AqlDevice *a = &g_aql[device];
+  if (!a->svc_launched.load(std::memory_order_acquire) || hsa_signal_load_relaxed(a->svc_sig) == 0) return;
+  std::unique_lock<std::mutex> lk(a->dq_mu, std::try_to_lock);
+  if (!lk.owns_lock() || a->svc_host[0] == a->svc_token) return;
+  volatile uint32_t *ctl = a->slab + (size_t)kSvcSlots * kSvcSlotWords;
+  if (a->slab_vram) _mm_sfence();
+  *ctl = ++a->ctl;
+  if (a->slab_vram) _mm_sfence();
+}
 void svc_atexit() {
   for (AqlDevice &a : g_aql) {
     if (!a.svc_host) continue;
@@ -3478,7 +3554,8 @@ int svc_ensure(AqlDevice *a) {
   };
   static_assert(sizeof(SvcArgs) == 32, "kernel-argument layout of mi_aql_dropin_svc");
   const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
-  const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8), a->svc_host_dev, token, dropin_svc_idle_ticks()};
+  const uint32_t idle = batch_busy() ? std::min(dropin_svc_idle_ticks(), 5000u) : dropin_svc_idle_ticks();  // 50 us
+  const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8), a->svc_host_dev, token, idle};
   hsa_signal_store_relaxed(a->svc_sig, 1);
   hsa_queue_t *q = dq_queue_locked(a, true);
   int rc = q ? dq_dispatch_locked(a, q, kAqlSvc, 1, kScalarThreads, &s, sizeof s, a->svc_karg, a->svc_sig) : -EIO;
@@ -3720,6 +3797,7 @@ int mi_cksum_chain_batch(const mi_chain_batch *b, uint16_t *out, void *stream) {
   const Shape sh = pick_shape(b->max_seg ? b->max_seg : 2048u);
   const int grid = grid_for(cd.n, sh.g);
   hipStream_t st = (hipStream_t)stream;
+  batch_activity(t_ctx.device);
   jnote("launch chain", nullptr, 0, (uint32_t)(sh.g * 100 + sh.u));
   jnote("  buffer", cd.base, cd.bytes, cd.n);
   jnote("  seg_off", cd.seg_off, 8ull * cd.nseg);
@@ -3745,6 +3823,26 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
   if (!d.n) return 0;
   return launch_verify(d, batch_max_len(b), ip_sum, l4_sum, status, bad_count,
                        (hipStream_t)stream);
+}
+
+// Experiment (tools/pareto_ranges.py, not in the public header): RX verify of
+// a packed batch with byte-balanced ranges -- wave w takes datagrams
+// [starts[w], starts[w+1]), at most 64 (starts: nr + 1 device words).
+int mi__verify_ranges(const mi_pkt_batch *b, const uint32_t *starts, uint32_t nr, uint16_t *ip_sum, uint16_t *l4_sum,
+                      uint8_t *status, uint32_t *bad_count, void *stream) {
+  Desc d;
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if ((rc = make_desc(b, &d))) return rc;
+  if (!d.n || !nr) return 0;
+  if (!starts || alloc_extent(starts, 4ull * (nr + 1u)) < 4ull * (nr + 1u))
+    return set_err(-EINVAL, "ranges: the starts array must hold nr + 1 words");
+  batch_activity(t_ctx.device);
+  jdesc("launch verify (ranges)", nr, d, ip_sum, l4_sum, status, bad_count);
+  const unsigned blocks = (nr + 1u) / 2u;
+  hipLaunchKernelGGL((k_ipv4_verify_ranges<8, 2>), dim3(blocks), dim3(128), 0, (hipStream_t)stream, d, ip_sum, l4_sum,
+                     status, bad_count, starts, nr);
+  return launched();
 }
 
 int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *ip, uint16_t *const *l4,
@@ -3788,6 +3886,7 @@ int mi_cksum_ipv4_verify_multi(const mi_pkt_batch *b, uint32_t nb, uint16_t *con
     a.e[k].st = status ? status[k] : nullptr;
     a.e[k].unit0 = units;
     jdesc(k ? "  multi batch" : "launch verify_multi", k, d[k], a.e[k].ip, a.e[k].l4, a.e[k].st, bad_count);
+    if (!k) batch_activity(t_ctx.device);
     const uint64_t u = ((uint64_t)d[k].n + gpw - 1) / gpw;
     if (units + u > 0xffffffffull) return set_err(-E2BIG, "too many datagrams in one launch");
     units += (uint32_t)u;
@@ -4651,7 +4750,7 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     return (uint32_t)(v < 0 ? 0 : v > (long)kSvcBurstMax ? kSvcBurstMax : v);
   }();
   int svc = 1;  // 0: the burst goes to the service
-  if (n && n <= burst_max && host_aql && dropin_svc_on() && aql_device(t_ctx.device, &adv) == 0 &&
+  if (n && n <= burst_max && host_aql && dropin_svc_on() && !batch_busy() && aql_device(t_ctx.device, &adv) == 0 &&
       (svc = svc_open(c, t_aql1)) < 0)
     return svc;
   if (svc == 0) {
@@ -4730,6 +4829,9 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
 // kernel of chunk k (PCIe-bound).  MI_CKSUM_HOST_ZC=0 forces
 // the staged path (MI_BATCH_HOST_STAGED per call).
 static int host_batch(const mi_pkt_batch *b, const HostOut &o, uint32_t *bad_count) {
+  // (host-memory bursts are latency work at the RX hook, not the HBM batch
+  // path the drop-in service stands aside for: batch_activity ignores them)
+  HostPath host_path;
   uint16_t *ip_sum = o.ip, *l4_sum = o.l4;
   uint8_t *status = o.st;
   int rc = ensure_ctx();
@@ -4906,6 +5008,7 @@ int mi_cksum_rx_offload_host(const mi_pkt_batch *b, uint32_t *csum_flags, uint32
 // TX copy + sums for frames in host memory (the driver's if_dpdk_transmit,
 // uinet_if_dpdk.c:583-597: socket-buffer chains -> hugepage rte_mbufs).
 int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags) {
+  HostPath host_path;  // (latency work at the TX hook: batch_activity ignores it)
   int rc = ensure_ctx();
   if (rc) return rc;
   if (!b) return set_err(-EINVAL, "batch is NULL");
@@ -5073,7 +5176,7 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   const bool aql = host_aql && aql_device(c.device, &adv) == 0;
   AqlOne &o = t_aql1;
   int svc = 1;  // 0: the service serves this call
-  if (aql && dropin_svc_on() && (svc = svc_open(c, o)) < 0) return svc;
+  if (aql && dropin_svc_on() && !batch_busy() && (svc = svc_open(c, o)) < 0) return svc;
   uint32_t wtag = tag;
   if (svc == 0) {
     volatile uint32_t *bx = svc_box(o);

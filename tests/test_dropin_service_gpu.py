@@ -241,3 +241,31 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
                 assert np.array_equal(fl, fl_all) and np.array_equal(cd, cd_all), (size, offs32)
     finally:
         mi.host_unregister(buf)
+
+
+def test_service_stands_aside_for_the_batch_path(lib):
+    """A batch submission stops the running service (its queue may share a
+    hardware pipe with the batch's: DESIGN.md 5.6), drop-ins within the quiet
+    time dispatch instead -- still right -- and the first drop-in after it
+    brings the service back."""
+    torch.cuda.init()
+    n, L = 4096, 1500
+    buf = torch.zeros(synth.IP_OFF + (n - 1) * synth.STRIDE_1500 + L + 64, dtype=torch.uint8, device="cuda")
+    b = mi.PktBatch(buf, n, stride=synth.STRIDE_1500, first_off=synth.IP_OFF, fixed_len=L)
+    mi.synth_ipv4(b, seed=5)
+    mi.ipv4_finalize(b)
+    torch.cuda.synchronize()
+    for _ in range(3):
+        time.sleep(0.002)  # past the quiet time of the last batch submission
+        assert mi.in_cksum_hdr(KAT_HDR, addr_mod=0) == 0x61B8
+        assert lib.mi__dropin_service_live() == 1
+        mi.ipv4_finalize(b)  # a batch submission
+        assert mi.in_cksum_hdr(KAT_HDR, addr_mod=1) == 0xB861  # inside the quiet time: a dispatch
+        deadline = time.monotonic() + 2.0
+        while lib.mi__dropin_service_live() and time.monotonic() < deadline:
+            time.sleep(0.0005)
+        assert lib.mi__dropin_service_live() == 0
+        torch.cuda.synchronize()
+        time.sleep(0.002)
+    assert mi.in_cksum_hdr(KAT_HDR, addr_mod=2) == 0x61B8
+    assert lib.mi__dropin_service_live() == 1

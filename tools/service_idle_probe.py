@@ -19,6 +19,8 @@ import os
 import sys
 import time
 
+# (the service must stay up beside the batch here: no standing aside)
+os.environ["MI_CKSUM_SERVICE_QUIET_US"] = "0"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 

@@ -15,7 +15,11 @@ one drop-in queue since round 5; a queue per thread before):
   calls_per_s        all drop-in threads together
   call_us_p50 / p99  one drop-in call's latency, over all threads' calls
 
-    python tools/service_interference.py [--seconds 2] > service_interference.jsonl
+Since round 5 the library keeps the service out of the way while its own
+batch path is busy (MI_CKSUM_SERVICE_QUIET_US): --quiet-us 0
+measures the service kept up beside the batch (set before the library loads).
+
+    python tools/service_interference.py [--seconds 2] [--quiet-us 0] > service_interference.jsonl
 """
 from __future__ import annotations
 
@@ -110,7 +114,10 @@ def main():
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--threads", default="1,4,16")
     ap.add_argument("--rotate", type=int, default=23)
+    ap.add_argument("--quiet-us", type=int, default=-1)
     a = ap.parse_args()
+    if a.quiet_us >= 0:
+        os.environ["MI_CKSUM_SERVICE_QUIET_US"] = str(a.quiet_us)
     lib = mi.load()
     lib.in_cksum_hdr.restype = C.c_uint
     lib.in_cksum_hdr.argtypes = [C.c_void_p]
@@ -134,7 +141,8 @@ def main():
             row = dict(mode=mode, dropin_threads=k, dropin_alone=solo, together=both,
                        batch_rate_vs_alone=round(both["batch_gib_s"] / alone["batch_gib_s"], 3),
                        dropin_calls_vs_alone=round(both["calls_per_s"] / solo["calls_per_s"], 3),
-                       service_slots_held=lib.mi__dropin_service_owners())
+                       service_slots_held=lib.mi__dropin_service_owners(),
+                       quiet_us=os.environ.get("MI_CKSUM_SERVICE_QUIET_US", "default"))
             print(json.dumps(row), flush=True)
     rep.close()
 
