@@ -2156,7 +2156,11 @@ int make_desc(const mi_pkt_batch *b, Desc *d) {
 
 // The journal entries of a launch over a batch (fault reporter): the launch,
 // then the arrays it references with their extents.
+struct AqlDevice;
 void batch_activity(int device);  // (the drop-in service stands aside)
+void batch_activity(AqlDevice *a);
+void batch_run_done();
+extern std::atomic<int> g_batch_runs;
 void jdesc(const char *what, uint32_t tag, const Desc &d, const void *ip = nullptr, const void *l4 = nullptr,
            const void *st = nullptr, const void *bad = nullptr) {
   jnote(what, nullptr, 0, tag);
@@ -3156,12 +3160,13 @@ int aql_wait(AqlRun *a) {
     }
   }
   a->pending = false;
+  batch_run_done();
   return 0;
 }
 
 // Submit `steps` passes starting with batch j0.
 int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
-  batch_activity(t_ctx.device);
+  batch_activity(a->dev);
   if (!steps) return 0;
   jnote("launch aql run", a->kargs, a->kargs_bytes, steps);
   const uint32_t nb = (uint32_t)(a->pkt.size() / a->nq);
@@ -3218,6 +3223,7 @@ int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
     if (written[q] && rung_idx[q] != last_idx[q]) ring(q);
   a->last_steps = steps;
   a->pending = true;
+  g_batch_runs.fetch_add(1, std::memory_order_relaxed);
   return 0;
 }
 
@@ -3478,27 +3484,37 @@ int64_t batch_quiet_ns() {
   }();
   return q;
 }
+// (prepared AQL runs in flight: the batch path is busy for their whole length,
+// not just the quiet time after their submission)
+std::atomic<int> g_batch_runs{0};
 bool batch_busy() {
   const int64_t q = batch_quiet_ns();
-  return q && now_ns() - g_batch_ns.load(std::memory_order_relaxed) < q;
+  return q && (g_batch_runs.load(std::memory_order_relaxed) > 0 ||
+               now_ns() - g_batch_ns.load(std::memory_order_relaxed) < q);
+}
+void batch_run_done() {
+  g_batch_runs.fetch_sub(1, std::memory_order_relaxed);
+  if (batch_quiet_ns()) g_batch_ns.store(now_ns(), std::memory_order_relaxed);
 }
 thread_local bool t_host_path = false;  // inside a host-memory batch call: not the batch path (PCIe-bound latency work)
 struct HostPath {
   HostPath() { t_host_path = true; }
   ~HostPath() { t_host_path = false; }
 };
-void batch_activity(int device) {
+void batch_activity(AqlDevice *a) {
   if (!batch_quiet_ns() || t_host_path) return;
   g_batch_ns.store(now_ns(), std::memory_order_relaxed);
-  if (device < 0 || device >= 64) return;
-  AqlDevice *a = &g_aql[device];
-  if (!a->svc_launched.load(std::memory_order_acquire) || hsa_signal_load_relaxed(a->svc_sig) == 0) return;
+  if (!a || !a->svc_launched.load(std::memory_order_acquire) || hsa_signal_load_relaxed(a->svc_sig) == 0) return;
   std::unique_lock<std::mutex> lk(a->dq_mu, std::try_to_lock);
   if (!lk.owns_lock() || a->svc_host[0] == a->svc_token) return;
   volatile uint32_t *ctl = a->slab + (size_t)kSvcSlots * kSvcSlotWords;
   if (a->slab_vram) _mm_sfence();
   *ctl = ++a->ctl;
   if (a->slab_vram) _mm_sfence();
+}
+void batch_activity(int device) {
+  if (device >= 0 && device < 64) batch_activity(&g_aql[device]);
+  else if (batch_quiet_ns() && !t_host_path) g_batch_ns.store(now_ns(), std::memory_order_relaxed);
 }
 void svc_atexit() {
   for (AqlDevice &a : g_aql) {
