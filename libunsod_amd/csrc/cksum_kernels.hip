@@ -3004,6 +3004,10 @@ void aql_leak(AqlRun *a) {
   g_live_queues.fetch_sub(nq);
   g_leaked_queues.fetch_add(nq);
   jnote("leak aql run", a->kargs, a->kargs_bytes, (uint32_t)nq);
+  if (a->pending) {  // (no longer counted as batch work in flight: the drop-in service may run again)
+    a->pending = false;
+    batch_run_done();
+  }
   fprintf(stderr, "libmicksum: AQL engine passes never completed (%s); the run's %d queue(s), signals and kernel "
           "arguments are leaked, not freed\n", t_err, nq);
 }
