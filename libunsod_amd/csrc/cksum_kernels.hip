@@ -2706,6 +2706,11 @@ struct AqlDevice {
   uint32_t *slab = nullptr, *slab_dev = nullptr;
   uint64_t slot_used = 0;
   uint32_t slot_seq[64] = {};
+  // queue placement (place_*): the library's queue creations on this device so
+  // far, the creation position (mod kPipes) of its first prepared handle's
+  // first queue and of the drop-in dispatch queue (the service queue follows it)
+  uint64_t qseq = 0;
+  int batch_pos = -1, dq_pos = -1;
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -2756,6 +2761,38 @@ void aql_queue_destroy(hsa_queue_t *&q) {
   g_live_queues.fetch_sub(1);
   q = nullptr;
 }
+// Queue placement.  A queue that holds work -- a resident
+// kernel, or a stream of dispatches -- on the same hardware pipe as a busy
+// batch queue costs that queue its overlap with the other (0.51-0.65x of the
+// 1500 B batch rate), and queues are dealt to four pipes round-robin in
+// creation order (tools/queue_place_probe.py: a resident wave on each of eight
+// queues created in a row after a batch pair costs nothing on 0, 1, 4, 5 and
+// 0.65x on 2, 3, 6, 7; profiles/r05/queue_place_probe_r05.jsonl).  The HSA API
+// does not name a queue's pipe, so the library places its own queues by
+// creation order: it counts the queues it creates on a device (under one lock,
+// so they are consecutive), and pads with spacer queues -- created and
+// destroyed at once, idle queues cost nothing -- so that the drop-in pair
+// (dispatch queue, service queue) takes the two pipes after the first prepared
+// handle's pair, and a later handle's pair the two pipes after the drop-in
+// pair.  Queues created by others in between (HIP streams) shift the real
+// positions; the library's own drop-in work creates HIP streams only on its
+// HIP fallback path.
+constexpr uint32_t kPipes = 4;
+std::mutex g_qplace_mu;
+std::atomic<int> g_spacer_err{0};
+int place_create(AqlDevice *a, uint32_t size, std::atomic<int> *err, hsa_queue_t **q) {  // (under g_qplace_mu)
+  const int rc = aql_queue_create(a->agent, size, err, q);
+  if (!rc) ++a->qseq;
+  return rc;
+}
+void place_pad(AqlDevice *a, uint32_t want) {  // (under g_qplace_mu)
+  for (uint32_t k = 0; k + 1 < kPipes && a->qseq % kPipes != want % kPipes; ++k) {
+    hsa_queue_t *q = nullptr;
+    if (place_create(a, 64, &g_spacer_err, &q)) return;
+    aql_queue_destroy(q);
+  }
+}
+
 double mono_s() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -3124,12 +3161,20 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     aql_free(a);
     return set_err(-EIO, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
   }
-  for (uint32_t q = 0; q < a->nq; ++q) {
-    if ((rc = aql_queue_create(dv->agent, 4096, &a->err, &a->q[q]))) {
-      aql_free(a);
-      return rc;
+  {
+    // (placement: the two pipes after the drop-in pair, or the first handle's)
+    std::lock_guard<std::mutex> lk(g_qplace_mu);
+    if (a->nq <= 2 && dv->dq_pos >= 0) place_pad(dv, (uint32_t)dv->dq_pos + 2u);
+    else if (a->nq <= 2 && dv->batch_pos >= 0) place_pad(dv, (uint32_t)dv->batch_pos);
+    const int pos = (int)(dv->qseq % kPipes);
+    for (uint32_t q = 0; q < a->nq; ++q) {
+      if ((rc = place_create(dv, 4096, &a->err, &a->q[q]))) {
+        aql_free(a);
+        return rc;
+      }
+      (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
     }
-    (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
+    if (dv->batch_pos < 0) dv->batch_pos = pos;
   }
   if (hsa_signal_create(0, 0, nullptr, &a->first) != HSA_STATUS_SUCCESS) {
     aql_free(a);
@@ -3403,10 +3448,18 @@ int dq_open(AqlDevice *a) {
 }
 // The dispatch queue (svc false) or the service's queue, created on first use
 // (under dq_mu); nullptr with the error set if it cannot be.
+// (the pair is created together, placed on the two pipes after the first
+// prepared handle's pair: place_*)
 hsa_queue_t *dq_queue_locked(AqlDevice *a, bool svc) {
-  hsa_queue_t *&q = svc ? a->sq : a->dq;
-  if (!q && aql_queue_create(a->agent, svc ? 64u : 256u, &a->dq_err, &q)) q = nullptr;
-  return q;
+  if (!a->dq) {
+    std::lock_guard<std::mutex> lk(g_qplace_mu);
+    if (a->batch_pos >= 0) place_pad(a, (uint32_t)a->batch_pos + 2u);
+    const int pos = (int)(a->qseq % kPipes);
+    if (place_create(a, 256u, &a->dq_err, &a->dq)) a->dq = nullptr;
+    if (a->dq && place_create(a, 64u, &a->dq_err, &a->sq)) a->sq = nullptr;
+    if (a->dq) a->dq_pos = pos;
+  }
+  return svc ? a->sq : a->dq;
 }
 
 // One dispatch packet into the device's drop-in queue.  The kernel arguments
@@ -4700,10 +4753,6 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     dbg_mem("zhost", c.zhost_dev, cap);
     c.zhost_cap = cap;
   }
-  if (!c.hstream[0])
-    for (int k = 0; k < ThreadCtx::kRing; ++k)
-      HIP_TRY(hipStreamCreateWithFlags(&c.hstream[k], hipStreamNonBlocking));
-  hipStream_t st = c.hstream[0];
   // layout (host view h, device view z): offs 8 n | lens 4 n | ip 2 n | l4 2 n | st n | flags 4 n | data 4 n
   uint8_t *h = c.zhost, *z = c.zhost_dev;
   const size_t o_lens = 8 * n, o_ip = 12 * n, o_l4 = 14 * n, o_st = 16 * n;
@@ -4825,6 +4874,12 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
     int rc = aql_one_submit(id, blocks, aql_wg(id), &args, sizeof args, true);
     if (rc) return rc;
   } else {
+    // (the HIP fallback: its streams only now -- a stream may create a queue,
+    // which shifts the library's queue placement, place_*)
+    if (!c.hstream[0])
+      for (int k = 0; k < ThreadCtx::kRing; ++k)
+        HIP_TRY(hipStreamCreateWithFlags(&c.hstream[k], hipStreamNonBlocking));
+    hipStream_t st = c.hstream[0];
     int rc = wide ? launch_verify_shape(d, Shape{64, 4}, zip, zl4, zst, zbad, st)
                   : launch_verify(d, max_len, zip, zl4, zst, zbad, st);
     if (rc) return rc;
@@ -5175,7 +5230,6 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
   ThreadCtx &c = t_ctx;
   if (!c.stage || off + len > c.stage_cap || c.stage_cap > kMaxBytes)
     return set_err(-EINVAL, "scalar staging overrun");
-  if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
   if ((rc = ensure_sout(c))) return rc;
   const uint32_t tag = next_tag(c);
   const bool trace = t_dtrace.on;
@@ -5226,6 +5280,8 @@ int mi__scalar_fold(size_t off, uint32_t len, uint32_t lanes, int pseudo, uint32
     // is gone: agent scope is only correct for fine-grained staging.)
     if ((rc = aql_one_submit(kAqlScalar, 1, kScalarThreads, &sa, sizeof sa, false))) return rc;
   } else {
+    // (the HIP fallback, MI_CKSUM_HOST_AQL=0: its stream only now, place_*)
+    if (!c.sstream) HIP_TRY(hipStreamCreateWithFlags(&c.sstream, hipStreamNonBlocking));
     hipLaunchKernelGGL(mi_aql_scalar, dim3(1), dim3(kScalarThreads), 0, c.sstream, (const uint8_t *)c.stage_dev,
                        (uint32_t)c.stage_cap, (uint32_t)off, len, lanes == MI_SPAN_ABS ? 1u : 0u, pseudo, src, dst,
                        (uint32_t)proto, plen, tag | (trace ? 0x80000000u : 0u), c.sout_dev);
