@@ -3523,22 +3523,29 @@ void svc_stop_locked(AqlDevice *a, double timeout_s) {
 // launch, a prepared run) notes the time and, if the device's service is
 // running, moves its control word (no wait: it leaves at its next idle poll,
 // and no new requests come -- a drop-in or small burst within the quiet time
-// of the latest submission dispatches instead, which leaves the batch
-// 0.90-0.96 of its rate); a service relaunched in that time (for a request
-// posted as it left) gets a short idle exit.  MI_CKSUM_SERVICE_QUIET_US
-// (default 500; 0: never stand aside).
+// of the latest submission dispatches instead); a service relaunched in that
+// time (for a request posted as it left) gets a short idle exit.  OFF by
+// default since the library places its queues (place_*): with the service's
+// queue on a pipe of its own, keeping it up beside the batch costs the batch
+// 2-5 % and keeps drop-ins at ~4 us, where standing aside costs 4-9 % and
+// ~13 us dispatches (profiles/r05/service_interference_placed_*.jsonl).  The
+// safety net for a process whose other queue creations defeat the placement:
+// MI_CKSUM_SERVICE_QUIET_US (or mi__set_service_quiet_us), e.g. 500.
 int64_t now_ns() {
   timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
 }
 std::atomic<int64_t> g_batch_ns{INT64_MIN / 2};
+std::atomic<int64_t> g_quiet_ns{-1};
 int64_t batch_quiet_ns() {
-  static const int64_t q = [] {
+  int64_t q = g_quiet_ns.load(std::memory_order_relaxed);
+  if (q < 0) {
     const char *e = getenv("MI_CKSUM_SERVICE_QUIET_US");
-    const long v = e ? atol(e) : 500L;
-    return (int64_t)(v > 0 ? v : 0) * 1000;
-  }();
+    const long v = e ? atol(e) : 0L;
+    q = (int64_t)(v > 0 ? v : 0) * 1000;
+    g_quiet_ns.store(q, std::memory_order_relaxed);
+  }
   return q;
 }
 // (prepared AQL runs in flight: the batch path is busy for their whole length,
@@ -5428,6 +5435,13 @@ int mi__spin_queue(uint32_t us, int k, int prio) {
   const uint64_t ticks = (uint64_t)us * 100u;
   uint8_t *ka = o.karg + 512u * (o.next++ % kAqlOneSlots);
   return dq_dispatch_locked(o.dev, qs[k], kAqlSpin, 1, 64, &ticks, sizeof ticks, ka, hsa_signal_t{0});
+}
+// Diagnostics / tests: the service's quiet time after a batch submission (us;
+// 0: it never stands aside), from now on; returns the previous value.
+long mi__set_service_quiet_us(long us) {
+  const long was = (long)(batch_quiet_ns() / 1000);
+  g_quiet_ns.store((int64_t)(us > 0 ? us : 0) * 1000, std::memory_order_relaxed);
+  return was;
 }
 // Is the drop-in service of the calling thread's device running?  (tests)
 int mi__dropin_service_live(void) {

@@ -244,11 +244,21 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
 
 
 def test_service_stands_aside_for_the_batch_path(lib):
-    """A batch submission stops the running service (its queue may share a
-    hardware pipe with the batch's: DESIGN.md 5.6), drop-ins within the quiet
-    time dispatch instead -- still right -- and the first drop-in after it
-    brings the service back."""
+    """With a quiet time set, a batch submission stops the running service
+    (the safety net for a queue placement other queue creations defeat:
+    DESIGN.md 5.6), drop-ins within the quiet time dispatch instead -- still
+    right -- and the first drop-in after it brings the service back."""
     torch.cuda.init()
+    lib.mi__set_service_quiet_us.restype = C.c_long
+    lib.mi__set_service_quiet_us.argtypes = [C.c_long]
+    was = lib.mi__set_service_quiet_us(500)  # (off by default: DESIGN.md 5.6)
+    try:
+        _stand_aside(lib)
+    finally:
+        lib.mi__set_service_quiet_us(was)
+
+
+def _stand_aside(lib):
     n, L = 4096, 1500
     buf = torch.zeros(synth.IP_OFF + (n - 1) * synth.STRIDE_1500 + L + 64, dtype=torch.uint8, device="cuda")
     b = mi.PktBatch(buf, n, stride=synth.STRIDE_1500, first_off=synth.IP_OFF, fixed_len=L)

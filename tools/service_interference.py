@@ -15,9 +15,9 @@ one drop-in queue since round 5; a queue per thread before):
   calls_per_s        all drop-in threads together
   call_us_p50 / p99  one drop-in call's latency, over all threads' calls
 
-Since round 5 the library keeps the service out of the way while its own
-batch path is busy (MI_CKSUM_SERVICE_QUIET_US): --quiet-us 0
-measures the service kept up beside the batch (set before the library loads).
+Round 5: the library can keep the service out of the way while its own batch
+path is busy (MI_CKSUM_SERVICE_QUIET_US, off by default since the library
+places its queues): --quiet-us 500 measures that.
 
     python tools/service_interference.py [--seconds 2] [--quiet-us 0] > service_interference.jsonl
 """
