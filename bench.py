@@ -561,7 +561,7 @@ def plumbing_64k(seconds: float = 1.0) -> dict:
 def dropin_latency(mi, calls: int = 400) -> dict:
     """(b1) drop-in cost per call on this host: libmicksum's in_cksum_hdr /
     in_cksum_pseudo_header / in_cksum_skip (the bytes read over PCIe from
-    pinned staging; one AQL dispatch per call, and through the thread's
+    pinned staging; one AQL dispatch per call, and through the device's
     resident drop-in service -- ``gpu_dropin_us`` is the library's default
     mode) against the reference's own functions (oracle/_ref) on the same real
     mbuf chains.  Median over `calls` calls through ctypes; ``ctypes_floor_us``
@@ -616,7 +616,7 @@ def dropin_latency(mi, calls: int = 400) -> dict:
     out["default_mode"] = "service" if default_mode else "dispatch"
 
     def both(g, args):
-        # one AQL dispatch per call, and the thread's resident drop-in service
+        # one AQL dispatch per call, and the device's resident drop-in service
         r = {}
         for mode, on in (("dispatch", 0), ("service", 1)):
             lib.mi__set_dropin_service(on)

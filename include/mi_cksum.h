@@ -11,14 +11,14 @@
  *       signatures -- they replace the MACHINE_SRCS object in_cksum.o inside
  *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  Each call
  *       gathers the mbuf chain into a per-thread pinned staging buffer and
- *       posts it to the thread's drop-in service -- one resident workgroup
- *       polling a mailbox in VRAM the host writes through the PCIe BAR (spans
- *       up to 2 KiB travel in the mailbox itself) -- then spins on a pinned
- *       result word: in_cksum_hdr ~2.9-3.1 us, a 1480-byte
- *       in_cksum_pseudo_header ~3.7-3.9 us per call on the MI355X host
- *       (MI_CKSUM_DROPIN_MAILBOX=host: mailbox in page-locked host
- *       memory, ~5 us; MI_CKSUM_DROPIN_SERVICE=0: one AQL dispatch per call,
- *       ~8 us).  This
+ *       posts it to the device's drop-in service -- one resident workgroup
+ *       for all threads, polling a mailbox slot per thread in VRAM the host
+ *       writes through the PCIe BAR (spans up to 2 KiB travel in the slot
+ *       itself) -- then spins on a pinned result word: in_cksum_hdr ~2.7-3.3
+ *       us, a 1480-byte in_cksum_pseudo_header ~3.3-4.0 us per call on the
+ *       MI355X host (MI_CKSUM_DROPIN_MAILBOX=host: slots in
+ *       page-locked host memory, ~5 us; MI_CKSUM_DROPIN_SERVICE=0: one AQL
+ *       dispatch per call, ~8 us).  This
  *       level is the compatibility path (the reference's call sites unchanged);
  *       per-packet RX/TX throughput comes from (b2) at the burst / inject-ring
  *       batch points.

@@ -2715,8 +2715,8 @@ struct AqlDevice {
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
 // HSA queues the library holds right now (diagnostics: mi_cksum_hsa_queues),
-// and those it gave up on: a thread's queue whose last dispatch never retired
-// (a GPU fault or hang) is leaked with everything the dispatch may still touch,
+// and those it gave up on: a prepared handle's queue whose passes never
+// completed (a GPU fault or hang) is leaked with everything the dispatch may still touch,
 // counted here instead of in g_live_queues (mi__hsa_queues_leaked)
 std::atomic<int> g_live_queues{0};
 std::atomic<int> g_leaked_queues{0};
@@ -3033,7 +3033,7 @@ void aql_free(AqlRun *a) {
 // queues, signals, kernel-argument block and the run object itself (its error
 // slot is the queues' callback data) are kept, not destroyed or freed under
 // dispatches that may still read them -- as aql_one_release does for a
-// thread's queue.  Counted in mi__hsa_queues_leaked, reported on stderr.
+// stuck thread's drop-in state.  Counted in mi__hsa_queues_leaked, reported on stderr.
 void aql_leak(AqlRun *a) {
   if (!a) return;
   int nq = 0;
@@ -4811,9 +4811,9 @@ static int verify_host_zero_copy(const mi_pkt_batch *b, const uint8_t *dbase, co
   unsigned blocks = 0;
   AqlDevice *adv = nullptr;
   // Bursts of at most MI_CKSUM_BURST_SERVICE_MAX datagrams (default 64, at
-  // most kSvcBurstMax; 0: never) go to the thread's drop-in service instead of
-  // a dispatch: the kernel arguments and the descriptors travel in its
-  // mailbox (VRAM, written through the BAR), one 8-lane group per datagram
+  // most kSvcBurstMax; 0: never) go to the device's drop-in service instead of
+  // a dispatch: the kernel arguments and the descriptors travel in the
+  // thread's mailbox slot (VRAM, written through the BAR), one 8-lane group per datagram
   // (64 at a time), and the service stores the result word once every output
   // is visible.  1500 B datagrams in host memory, median per burst
   // (profiles/r04/burst_service_lanes_r04.jsonl, burst_dispatch_r04.jsonl):
@@ -5222,10 +5222,11 @@ uint8_t *mi__scalar_staging(size_t need) {
 // One (b1) fold.  The kernel stores (tag << 16) | sum into the pinned slot
 // with a system-scope store and the host spins on the slot (a few us sooner
 // than a completion signal).  Either one dispatch per call (mi_aql_scalar: an
-// AQL packet into the thread's queue, or with MI_CKSUM_HOST_AQL=0 a HIP
-// launch), or, with the drop-in service on, a request into the mailbox of the
-// thread's resident mi_aql_dropin_svc workgroup (launched by the first call and
-// again whenever it has retired on its idle exit).  The spin also watches the
+// AQL packet into the device's drop-in dispatch queue, or with
+// MI_CKSUM_HOST_AQL=0 a HIP launch), or, with the drop-in service on, a request
+// into the thread's mailbox slot of the device's resident mi_aql_dropin_svc
+// workgroup (launched by a first call and again whenever it has retired on its
+// idle exit).  The spin also watches the
 // work itself: a kernel that retires without storing the word, a queue error
 // or a 10 s wall-clock deadline end the call with an error, never a hang; a
 // slow GPU (busy, time-sliced) only makes the call slower.

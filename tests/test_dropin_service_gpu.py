@@ -210,8 +210,8 @@ def test_breakdown_stamps(lib, service):
 
 
 def test_small_host_bursts_through_the_service(lib, demux_golden):
-    """Host-memory bursts of at most 64 datagrams go to the thread's service
-    (arguments and descriptors in its mailbox), larger ones to a dispatch:
+    """Host-memory bursts of at most 64 datagrams go to the device's service
+    (arguments and descriptors in the thread's mailbox slot), larger ones to a dispatch:
     the reference-generated demux golden (TCP / UDP / ICMP / IGMP / CARP,
     options, fragments, bad sums, malformed headers) in bursts of 1-128 must
     give the golden ip / l4 / status and the same RX offload flags as one
