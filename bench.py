@@ -325,9 +325,10 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
     config = wl.get("name", args.config)
     traffic, tsrc = None, None
     # HBM bytes per launch from the newest PMC record of this config (request-
-    # size counters, rounds 3-4; FETCH_SIZE x2, round 2), labelled with its source
+    # size counters, rounds 3-5; FETCH_SIZE x2, round 2), labelled with its source
     tkey = config + ("_u64" if args.offs64 else "_u32") if config == "pareto" else config
-    for rel in ("profiles/r04/pmc_traffic_r04.json", "profiles/r03/pmc_traffic_r03.json", "profiles/pmc_traffic_r02.json"):
+    for rel in ("profiles/r05/pmc_traffic_r05.json", "profiles/r04/pmc_traffic_r04.json", "profiles/r03/pmc_traffic_r03.json",
+                "profiles/pmc_traffic_r02.json"):
         tfile = os.path.join(ROOT, rel)
         try:
             ent = json.load(open(tfile)).get(tkey) if os.path.exists(tfile) else None
