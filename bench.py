@@ -48,6 +48,10 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (RCCL) even for one rank: rehearses the N>1 path's "
+                         "process group, barrier, max-over-ranks and per-GPU all_gather on a one-GPU box "
+                         "(launch under torch.distributed.run --nproc-per-node 1)")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--config", default="1500", choices=list(CONFIGS) + ["pareto"])
@@ -391,7 +395,7 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)

@@ -54,7 +54,7 @@ def job_totals(elapsed_s: float, nbytes: float, npkts: float, device=None) -> tu
     None = CPU for gloo)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return float(elapsed_s), float(nbytes), float(npkts)
     t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
