@@ -1553,10 +1553,11 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_scalar(const
 // (bytes, device address) and [kBoxOut] its result block; [kSvcInline..] a
 // span of at most kSvcInlineBytes staging bytes (offset included), or a
 // burst's arguments and descriptors.  Wave 0 polls every slot's sequence word
-// and the control word with ONE load per lane; a slot whose word moved is
-// served (fields and inline chunks with one round trip; an inline span by wave
-// 0 alone, a staged span or a burst by the whole workgroup), acknowledged, and
-// its result stored into the thread's result block as mi_aql_scalar stores it.
+// and the control word with ONE load per lane; the slots whose word moved are
+// served round robin (fields and inline chunks with one round trip; an inline
+// span by wave 0 alone, a staged span or a burst by the whole workgroup),
+// acknowledged, and the result stored into the thread's result block as
+// mi_aql_scalar stores it.
 // Exit conditions every wave reaches: the control word moves (process exit),
 // or no slot moved for idle_ticks of the 100 MHz clock -- the next caller sees
 // the dispatch retire (its completion signal) and launches a new one, which
@@ -1630,6 +1631,7 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
     last = lane < ns ? ld_u32<kSys | kVolatile>(mb, lane * kSvcSlotWords + kBoxAck)
                      : ld_u32<kSys | kVolatile>(mb, my_word);
   uint64_t t_last = rt_clock(), t_seen = 0;
+  uint32_t rr = 0;  // wave 0: the slot after the last one served
   for (;;) {
     if (threadIdx.x < 64) {
       uint32_t w = 0, s = ~0u;
@@ -1639,7 +1641,11 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
         const uint64_t pend = __ballot(lane < ns && w != last);
         stop = __builtin_amdgcn_readlane((int)(w ^ last), 63) != 0;
         if (pend) {
-          s = (uint32_t)__builtin_ctzll(pend);
+          // round robin: the first pending slot after the one served last (a
+          // thread that posts again at once does not starve the others)
+          const uint64_t after = pend & (~0ull << rr);
+          s = (uint32_t)__builtin_ctzll(after ? after : pend);
+          rr = s + 1u;
           break;
         }
         if (stop || rt_clock() - t_last > idle_ticks) break;
