@@ -2712,11 +2712,10 @@ struct AqlDevice {
   uint32_t *slab = nullptr, *slab_dev = nullptr;
   uint64_t slot_used = 0;
   uint32_t slot_seq[64] = {};
-  // queue placement (place_*): the library's queue creations on this device so
-  // far, the creation position (mod kPipes) of its first prepared handle's
-  // first queue and of the drop-in dispatch queue (the service queue follows it)
-  uint64_t qseq = 0;
-  int batch_pos = -1, dq_pos = -1;
+  // queue placement (place_create): the id classes (id mod kPipes, a bit each)
+  // the prepared handles' queues and the drop-in queues took (the drop-in
+  // queues avoid the handles' classes)
+  uint32_t batch_mask = 0, dropin_mask = 0;
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -2770,32 +2769,42 @@ void aql_queue_destroy(hsa_queue_t *&q) {
 // Queue placement.  A queue that holds work -- a resident
 // kernel, or a stream of dispatches -- on the same hardware pipe as a busy
 // batch queue costs that queue its overlap with the other (0.51-0.65x of the
-// 1500 B batch rate), and queues are dealt to four pipes round-robin in
-// creation order (tools/queue_place_probe.py: a resident wave on each of eight
-// queues created in a row after a batch pair costs nothing on 0, 1, 4, 5 and
-// 0.65x on 2, 3, 6, 7; profiles/r05/queue_place_probe_r05.jsonl).  The HSA API
-// does not name a queue's pipe, so the library places its own queues by
-// creation order: it counts the queues it creates on a device (under one lock,
-// so they are consecutive), and pads with spacer queues -- created and
-// destroyed at once, idle queues cost nothing -- so that the drop-in pair
-// (dispatch queue, service queue) takes the two pipes after the first prepared
-// handle's pair, and a later handle's pair the two pipes after the drop-in
-// pair.  Queues created by others in between (HIP streams) shift the real
-// positions; the library's own drop-in work creates HIP streams only on its
-// HIP fallback path.
+// 1500 B batch rate).  The HSA API does not name a queue's pipe; what the
+// measurements show is that queues are dealt to four pipes in the order they
+// exist: tools/queue_place_probe.py put a resident wave on eight queues
+// created after a batch pair, with and without a foreign queue created in
+// between, and (id - the batch queue's id) mod 4 -- ROCr numbers the process's
+// queues in creation order, HIP's and anyone else's included -- named every
+// one of the 16 that cost the batch 0.65x (profiles/r05/
+// queue_place_probe_ids_r05.jsonl); a queue created to replace a destroyed
+// one does NOT take the destroyed one's class (service_idle_probe_destroyed_retry_r05.jsonl).
+// So the library creates its drop-in queues in id classes its prepared batch
+// handles' queues do not use (a handle created later lands after them, in
+// other classes, by itself); a drop-in queue that lands in a class it must
+// avoid is kept as an idle spacer (never destroyed: destroying would move
+// every later queue) and another created -- at most three spacers per queue,
+// once per device; idle queues cost nothing (queue_probe_r05.jsonl, up to 8).
+// Spacers are not counted in mi_cksum_hsa_queues.  A queue destroyed later by
+// anyone (a closed handle, another component) shifts the classes of the
+// queues after it; the stand-aside (MI_CKSUM_SERVICE_QUIET_US) is the fallback
+// for such processes.
 constexpr uint32_t kPipes = 4;
 std::mutex g_qplace_mu;
-std::atomic<int> g_spacer_err{0};
-int place_create(AqlDevice *a, uint32_t size, std::atomic<int> *err, hsa_queue_t **q) {  // (under g_qplace_mu)
-  const int rc = aql_queue_create(a->agent, size, err, q);
-  if (!rc) ++a->qseq;
-  return rc;
-}
-void place_pad(AqlDevice *a, uint32_t want) {  // (under g_qplace_mu)
-  for (uint32_t k = 0; k + 1 < kPipes && a->qseq % kPipes != want % kPipes; ++k) {
-    hsa_queue_t *q = nullptr;
-    if (place_create(a, 64, &g_spacer_err, &q)) return;
-    aql_queue_destroy(q);
+std::atomic<int> g_spacer_queues{0};  // (diagnostics: mi__placement_spacers)
+// Create a queue whose id class (id mod kPipes) is not in `avoid` (a bit per
+// class); returns its class, or -1 with the error set.  (under g_qplace_mu)
+int place_create(AqlDevice *a, uint32_t size, std::atomic<int> *err, hsa_queue_t **q, uint32_t avoid) {
+  for (uint32_t spacers = 0;; ++spacers) {
+    if (aql_queue_create(a->agent, size, err, q)) return -1;
+    const uint32_t c = (uint32_t)((*q)->id % kPipes);
+    if (!(avoid >> c & 1u) || spacers + 1 >= kPipes) return (int)c;
+    // (kept, idle -- no packet is ever written to it -- for the process's
+    // life; only the drop-in queues are placed this way, and their error slot
+    // lives as long as the device state)
+    if (debug_queues()) fprintf(stderr, "libmicksum: HSA queue %p kept as a placement spacer\n", (void *)*q);
+    g_live_queues.fetch_sub(1);
+    g_spacer_queues.fetch_add(1);
+    *q = nullptr;
   }
 }
 
@@ -3168,19 +3177,16 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     return set_err(-EIO, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
   }
   {
-    // (placement: the two pipes after the drop-in pair, or the first handle's)
+    // (placement: the drop-in queues, created later, avoid these classes)
     std::lock_guard<std::mutex> lk(g_qplace_mu);
-    if (a->nq <= 2 && dv->dq_pos >= 0) place_pad(dv, (uint32_t)dv->dq_pos + 2u);
-    else if (a->nq <= 2 && dv->batch_pos >= 0) place_pad(dv, (uint32_t)dv->batch_pos);
-    const int pos = (int)(dv->qseq % kPipes);
     for (uint32_t q = 0; q < a->nq; ++q) {
-      if ((rc = place_create(dv, 4096, &a->err, &a->q[q]))) {
+      if ((rc = aql_queue_create(dv->agent, 4096, &a->err, &a->q[q]))) {
         aql_free(a);
         return rc;
       }
+      dv->batch_mask |= 1u << (uint32_t)(a->q[q]->id % kPipes);
       (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
     }
-    if (dv->batch_pos < 0) dv->batch_pos = pos;
   }
   if (hsa_signal_create(0, 0, nullptr, &a->first) != HSA_STATUS_SUCCESS) {
     aql_free(a);
@@ -3454,16 +3460,20 @@ int dq_open(AqlDevice *a) {
 }
 // The dispatch queue (svc false) or the service's queue, created on first use
 // (under dq_mu); nullptr with the error set if it cannot be.
-// (the pair is created together, placed on the two pipes after the first
-// prepared handle's pair: place_*)
+// (the pair is created together, off the prepared handles' pipes and, where
+// a pipe is left, apart from each other: place_create)
 hsa_queue_t *dq_queue_locked(AqlDevice *a, bool svc) {
   if (!a->dq) {
     std::lock_guard<std::mutex> lk(g_qplace_mu);
-    if (a->batch_pos >= 0) place_pad(a, (uint32_t)a->batch_pos + 2u);
-    const int pos = (int)(a->qseq % kPipes);
-    if (place_create(a, 256u, &a->dq_err, &a->dq)) a->dq = nullptr;
-    if (a->dq && place_create(a, 64u, &a->dq_err, &a->sq)) a->sq = nullptr;
-    if (a->dq) a->dq_pos = pos;
+    const int cd = place_create(a, 256u, &a->dq_err, &a->dq, a->batch_mask);
+    if (cd < 0) {
+      a->dq = nullptr;
+    } else {
+      const uint32_t both = a->batch_mask | 1u << cd;
+      const int cs = place_create(a, 64u, &a->dq_err, &a->sq, both == 0xfu ? a->batch_mask : both);
+      if (cs < 0) a->sq = nullptr;
+      a->dropin_mask = 1u << cd | (cs >= 0 ? 1u << cs : 0u);
+    }
   }
   return svc ? a->sq : a->dq;
 }
@@ -5427,8 +5437,10 @@ int mi__spin(uint32_t us, int via) {
 // microseconds on the k-th of up to 16 extra queues of the calling thread's
 // device (created in order on first use, 64 packets; prio >= 0: set the
 // queue's priority first, 0 low .. 2 high).
+static hsa_queue_t *g_spin_qs[16];
+long long mi__spin_queue_id(int k) { return k >= 0 && k < 16 && g_spin_qs[k] ? (long long)g_spin_qs[k]->id : -1; }
 int mi__spin_queue(uint32_t us, int k, int prio) {
-  static hsa_queue_t *qs[16];
+  hsa_queue_t **qs = g_spin_qs;
   static std::atomic<int> qerr{0};
   if (k < 0 || k >= 16) return set_err(-EINVAL, "queue index");
   int rc = ensure_ctx();
@@ -5450,6 +5462,21 @@ long mi__set_service_quiet_us(long us) {
   g_quiet_ns.store((int64_t)(us > 0 ? us : 0) * 1000, std::memory_order_relaxed);
   return was;
 }
+// Diagnostics (tools/queue_place_probe.py): the HSA queue ids (ROCr numbers
+// every queue of the process in creation order, HIP's own included) of extra
+// queue k (mi__spin_queue), of a prepared handle's queue i, and of the
+// device's drop-in dispatch (0) / service (1) queue; -1 if there is none.
+long long mi__spin_queue_id(int k);
+long long mi__repeat_queue_id(const mi_repeat *r, int i) {
+  return r && r->aql && i >= 0 && i < 4 && r->aql->q[i] ? (long long)r->aql->q[i]->id : -1;
+}
+long long mi__dropin_queue_id(int which) {
+  const AqlDevice *a = t_aql1.dev;
+  const hsa_queue_t *q = !a ? nullptr : which ? a->sq : a->dq;
+  return q ? (long long)q->id : -1;
+}
+// Diagnostics: idle spacer queues kept by the queue placement (place_create).
+int mi__placement_spacers(void) { return g_spacer_queues.load(); }
 // Is the drop-in service of the calling thread's device running?  (tests)
 int mi__dropin_service_live(void) {
   const AqlDevice *a = t_aql1.dev;

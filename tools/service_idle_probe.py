@@ -78,12 +78,18 @@ def main():
     print(json.dumps(dict(case="no service", batch_gib_s=base)), flush=True)
     # any resident wave, no memory traffic: via a HIP stream, the service's
     # queue, the drop-in dispatch queue
+    lib.mi__dropin_queue_id.restype = C.c_longlong
+    lib.mi__dropin_queue_id.argtypes = [C.c_int]
+    lib.mi__repeat_queue_id.restype = C.c_longlong
+    lib.mi__repeat_queue_id.argtypes = [C.c_void_p, C.c_int]
     for via, name in ((0, "HIP stream"), (1, "service queue"), (2, "dispatch queue")):
         assert lib.mi__spin(2_500_000, via) == 0
         time.sleep(0.1)
         r = rate()
-        print(json.dumps(dict(case="resident spin wave", via=name, batch_gib_s=r, batch_vs_none=round(r / base, 3))),
-              flush=True)
+        print(json.dumps(dict(case="resident spin wave", via=name, batch_gib_s=r, batch_vs_none=round(r / base, 3),
+                              batch_queue_ids=[lib.mi__repeat_queue_id(rep._h, i) for i in (0, 1)],
+                              dropin_queue_ids=[lib.mi__dropin_queue_id(0), lib.mi__dropin_queue_id(1)],
+                              spacers=lib.mi__placement_spacers())), flush=True)
         time.sleep(1.0)  # (the spin ends)
     # one queue for the batch side, with and without the service
     rep1 = mi.VerifyRepeat(bs, outs, nstreams=1, engine="aql")
