@@ -2785,7 +2785,7 @@ void aql_queue_destroy(hsa_queue_t *&q) {
 // every later queue) and another created -- at most three spacers per queue,
 // once per device; idle queues cost nothing (queue_probe_r05.jsonl, up to 8).
 // Spacers are not counted in mi_cksum_hsa_queues.  A queue destroyed later by
-// anyone (a closed handle, another component) shifts the classes of the
+// anyone (a closed handle, another component) may shift the classes of the
 // queues after it; the stand-aside (MI_CKSUM_SERVICE_QUIET_US) is the fallback
 // for such processes.
 constexpr uint32_t kPipes = 4;
