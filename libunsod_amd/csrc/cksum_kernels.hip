@@ -2715,7 +2715,12 @@ struct AqlDevice {
   // queue placement (place_create): the id classes (id mod kPipes, a bit each)
   // the prepared handles' queues and the drop-in queues took (the drop-in
   // queues avoid the handles' classes)
-  uint32_t batch_mask = 0, dropin_mask = 0;
+  uint32_t batch_cnt[4] = {}, dropin_mask = 0;  // live prepared-handle queues per class
+  uint32_t batch_mask() const {
+    uint32_t m = 0;
+    for (uint32_t c = 0; c < 4; ++c) m |= batch_cnt[c] ? 1u << c : 0u;
+    return m == 0xfu ? 0u : m;  // (every class taken: nothing to avoid)
+  }
 };
 std::mutex g_aql_mu;
 AqlDevice g_aql[64];
@@ -3033,7 +3038,13 @@ struct AqlRun {
 
 void aql_free(AqlRun *a) {
   if (!a) return;
-  for (auto *&q : a->q) aql_queue_destroy(q);
+  for (auto *&q : a->q) {
+    if (q && a->dev) {
+      std::lock_guard<std::mutex> lk(g_qplace_mu);
+      --a->dev->batch_cnt[q->id % kPipes];
+    }
+    aql_queue_destroy(q);
+  }
   if (a->have_first) (void)hsa_signal_destroy(a->first);
   if (a->have_rest) (void)hsa_signal_destroy(a->rest);
   if (a->kargs) {
@@ -3184,7 +3195,7 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
         aql_free(a);
         return rc;
       }
-      dv->batch_mask |= 1u << (uint32_t)(a->q[q]->id % kPipes);
+      ++dv->batch_cnt[a->q[q]->id % kPipes];
       (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
     }
   }
@@ -3465,12 +3476,13 @@ int dq_open(AqlDevice *a) {
 hsa_queue_t *dq_queue_locked(AqlDevice *a, bool svc) {
   if (!a->dq) {
     std::lock_guard<std::mutex> lk(g_qplace_mu);
-    const int cd = place_create(a, 256u, &a->dq_err, &a->dq, a->batch_mask);
+    const uint32_t bm = a->batch_mask();
+    const int cd = place_create(a, 256u, &a->dq_err, &a->dq, bm);
     if (cd < 0) {
       a->dq = nullptr;
     } else {
-      const uint32_t both = a->batch_mask | 1u << cd;
-      const int cs = place_create(a, 64u, &a->dq_err, &a->sq, both == 0xfu ? a->batch_mask : both);
+      const uint32_t both = bm | 1u << cd;
+      const int cs = place_create(a, 64u, &a->dq_err, &a->sq, both == 0xfu ? bm : both);
       if (cs < 0) a->sq = nullptr;
       a->dropin_mask = 1u << cd | (cs >= 0 ? 1u << cs : 0u);
     }
