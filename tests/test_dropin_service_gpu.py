@@ -279,3 +279,47 @@ def _stand_aside(lib):
         time.sleep(0.002)
     assert mi.in_cksum_hdr(KAT_HDR, addr_mod=2) == 0x61B8
     assert lib.mi__dropin_service_live() == 1
+
+
+def test_dropin_queues_avoid_the_batch_queues_pipes():
+    """Queue placement: in a fresh process, a prepared batch
+    handle's two queues, then a foreign queue (a HIP stream's), then the
+    drop-in queues -- which must land in HSA queue-id classes (mod 4) the
+    batch queues do not use, spacers taking the rejected ids."""
+    import os
+    import subprocess
+    import sys
+    code = r"""
+import ctypes as C, json, torch
+import libunsod_amd as mi
+from libunsod_amd import synth
+lib = mi.load()
+for f in ("mi__repeat_queue_id", "mi__dropin_queue_id"):
+    getattr(lib, f).restype = C.c_longlong
+lib.mi__repeat_queue_id.argtypes = [C.c_void_p, C.c_int]
+lib.mi__dropin_queue_id.argtypes = [C.c_int]
+n, L = 1024, 1500
+buf = torch.zeros(synth.IP_OFF + (n - 1) * synth.STRIDE_1500 + L + 64, dtype=torch.uint8, device="cuda")
+b = mi.PktBatch(buf, n, stride=synth.STRIDE_1500, first_off=synth.IP_OFF, fixed_len=L)
+mi.synth_ipv4(b, seed=1); mi.ipv4_finalize(b); torch.cuda.synchronize()
+rep = mi.VerifyRepeat([b], [dict(status=torch.empty(n, dtype=torch.uint8, device="cuda"))], nstreams=2, engine="aql")
+rep.run(4)
+s = torch.cuda.Stream(); x = torch.ones(16, device="cuda")
+with torch.cuda.stream(s): x.add_(1)
+torch.cuda.synchronize()
+assert mi.in_cksum_hdr(bytes.fromhex("450000730000400040110000c0a80001c0a800c7")) == 0x61B8
+print(json.dumps(dict(batch=[lib.mi__repeat_queue_id(rep._h, i) for i in (0, 1)],
+                      dropin=[lib.mi__dropin_queue_id(0), lib.mi__dropin_queue_id(1)],
+                      spacers=lib.mi__placement_spacers())))
+rep.close()
+"""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    batch = {q % 4 for q in got["batch"]}
+    dq, sq = got["dropin"]
+    assert min(got["batch"]) >= 0 and dq >= 0 and sq >= 0, got
+    assert dq % 4 not in batch and sq % 4 not in batch, got
+    print("queue ids:", got)
