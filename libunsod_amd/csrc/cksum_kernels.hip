@@ -354,7 +354,8 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes,
-                                            const uint32_t *starts = nullptr, uint32_t nr = 0) {
+                                            const uint32_t *starts = nullptr, uint32_t nr = 0,
+                                            const uint32_t *ends = nullptr) {
   constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[NW][W];
@@ -369,8 +370,10 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
   if constexpr (RG) {
     const uint32_t w = blockIdx.x * NW + wv;
     if (w >= nr) return;
-    const Arr sa = arr_of(starts, 4ull * (nr + 1u));
-    const uint32_t b = lane < 2u ? ld_u32(sa, w + lane) : 0u;
+    // (ends: wave w's range ends at ends[w], so the ranges may come in any
+    // order; without, at starts[w + 1])
+    const Arr sa = arr_of(starts, 4ull * (ends ? nr : nr + 1u)), ea = arr_of(ends, 4ull * nr);
+    const uint32_t b = lane == 0u ? ld_u32(sa, w) : lane == 1u ? (ends ? ld_u32(ea, w) : ld_u32(sa, w + 1u)) : 0u;
     p0 = (uint32_t)__builtin_amdgcn_readlane((int)b, 0);
     const uint32_t p1 = (uint32_t)__builtin_amdgcn_readlane((int)b, 1);
     cnt = p1 > p0 ? min(p1 - p0, 64u) : 0u;
@@ -570,8 +573,8 @@ __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Des
 template <int U, int NW>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_ranges(Desc d, uint16_t *ip_out, uint16_t *l4_out,
                                                                 uint8_t *st_out, uint32_t *bad, const uint32_t *starts,
-                                                                uint32_t nr) {
-  packed_body<U, 0, NW, true>(d, ip_out, l4_out, st_out, bad, SpanSeeds{}, 0u, starts, nr);
+                                                                uint32_t nr, const uint32_t *ends) {
+  packed_body<U, 0, NW, true>(d, ip_out, l4_out, st_out, bad, SpanSeeds{}, 0u, starts, nr, ends);
 }
 
 // The bounds of a wave's 64-datagram range (the flat-run kernels): the run
@@ -3936,20 +3939,23 @@ int mi_cksum_ipv4_verify(const mi_pkt_batch *b, uint16_t *ip_sum, uint16_t *l4_s
 // Experiment (tools/pareto_ranges.py, not in the public header): RX verify of
 // a packed batch with byte-balanced ranges -- wave w takes datagrams
 // [starts[w], starts[w+1]), at most 64 (starts: nr + 1 device words).
+// ends (may be NULL): wave w's range is [starts[w], ends[w]) -- ranges in any
+// order (nr words each; starts then needs only nr).
 int mi__verify_ranges(const mi_pkt_batch *b, const uint32_t *starts, uint32_t nr, uint16_t *ip_sum, uint16_t *l4_sum,
-                      uint8_t *status, uint32_t *bad_count, void *stream) {
+                      uint8_t *status, uint32_t *bad_count, void *stream, const uint32_t *ends) {
   Desc d;
   int rc = ensure_ctx();
   if (rc) return rc;
   if ((rc = make_desc(b, &d))) return rc;
   if (!d.n || !nr) return 0;
-  if (!starts || alloc_extent(starts, 4ull * (nr + 1u)) < 4ull * (nr + 1u))
-    return set_err(-EINVAL, "ranges: the starts array must hold nr + 1 words");
+  const uint64_t need = 4ull * (ends ? nr : nr + 1u);
+  if (!starts || alloc_extent(starts, need) < need || (ends && alloc_extent(ends, 4ull * nr) < 4ull * nr))
+    return set_err(-EINVAL, "ranges: starts must hold nr + 1 words (nr with ends), ends nr");
   batch_activity(t_ctx.device);
   jdesc("launch verify (ranges)", nr, d, ip_sum, l4_sum, status, bad_count);
   const unsigned blocks = (nr + 1u) / 2u;
   hipLaunchKernelGGL((k_ipv4_verify_ranges<8, 2>), dim3(blocks), dim3(128), 0, (hipStream_t)stream, d, ip_sum, l4_sum,
-                     status, bad_count, starts, nr);
+                     status, bad_count, starts, nr, ends);
   return launched();
 }
 

@@ -13,7 +13,9 @@ build it on the GPU inside the timed region):
   greedy  close a range when it holds >= T bytes or 64 datagrams;
   bucket  cut at every multiple of T of the running byte count and every
           64th datagram after such a cut (a rule a GPU pass can apply per
-          datagram with no scan).
+          datagram with no scan);
+  lpt     the same ranges dispatched heaviest first (list scheduling's
+          longest-processing-time order).
 
 T runs over multiples of the mean 64-datagram range.  Each case's outputs
 are checked equal to the default kernel's.  One JSON line per case.
@@ -72,7 +74,7 @@ def main():
     a = ap.parse_args()
     lib = mi.load()
     lib.mi__verify_ranges.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
-                                      C.c_void_p, C.c_void_p]
+                                      C.c_void_p, C.c_void_p, C.c_void_p]
     dev = torch.device("cuda", 0)
     n = 1 << 22
     lens = synth.pareto_lengths(n)
@@ -115,6 +117,34 @@ def main():
     byts = np.add.reduceat(lens.astype(np.int64), np.arange(0, n, 64))
     print(json.dumps(dict(case="range bytes, default", mean=round(float(byts.mean())), std=round(float(byts.std())),
                           max=int(byts.max()))), flush=True)
+    # longest first: the default 64-datagram ranges (and greedy 1.25x ones),
+    # dispatched heaviest first -- list scheduling's LPT order (ranges in any
+    # order through an explicit end per range)
+    for kind, st in (("lpt, 64-datagram ranges", np.arange(0, n + 1, 64, dtype=np.int64)),
+                     ("lpt, greedy 1.25x", greedy(lens, mean64 * 1.25).astype(np.int64))):
+        rb = np.add.reduceat(lens.astype(np.int64), st[:-1])
+        order = np.argsort(-rb, kind="stable")
+        s0 = torch.from_numpy(st[:-1][order].astype(np.int32)).to(dev)
+        e0 = torch.from_numpy(st[1:][order].astype(np.int32)).to(dev)
+        nr = len(order)
+
+        def lpt(j, s, s0=s0, e0=e0, nr=nr):
+            o = outs[j]
+            check("ranges", lib.mi__verify_ranges(C.byref(bs[j].c), s0.data_ptr(), nr, o["ip"].data_ptr(),
+                                                  o["l4"].data_ptr(), o["status"].data_ptr(), None,
+                                                  C.c_void_p(s.cuda_stream), e0.data_ptr()))
+
+        for o in outs:
+            for v in o.values():
+                v.fill_(0xA5)
+        run(lpt, a.rotate)
+        same = all(torch.equal(outs[j][k], ref[j][k]) for j in range(a.rotate) for k in ref[j])
+        t = [round(run(lpt, a.steps), 2) for _ in range(2)]
+        print(json.dumps(dict(case=kind, waves=nr, outputs_equal=same, us_per_launch=t,
+                              frac=round(alg / (min(t) * 1e-6) / 8e12, 4), vs_default=round(min(t_base) / min(t), 3))),
+              flush=True)
+        if not same:
+            raise SystemExit("outputs differ")
     for kind, fn in (("greedy", greedy), ("bucket", bucket)):
         for f in (0.75, 1.0, 1.25, 1.5):
             T = mean64 * f
@@ -129,7 +159,7 @@ def main():
                 o = outs[j]
                 check("ranges", lib.mi__verify_ranges(C.byref(bs[j].c), sdev.data_ptr(), nr, o["ip"].data_ptr(),
                                                       o["l4"].data_ptr(), o["status"].data_ptr(), None,
-                                                      C.c_void_p(s.cuda_stream)))
+                                                      C.c_void_p(s.cuda_stream), None))
 
             for o in outs:
                 for v in o.values():
