@@ -1612,19 +1612,59 @@ __device__ __forceinline__ void svc_burst(const BurstArgs &a) {
           a.l4, a.st, a.bad, d);
   }
 }
+// One inline request (slot s, sequence word sq) served by the calling wave:
+// the slot's fields and inline bytes with one round trip (no acquire fence:
+// system-scope loads of the slot, issued after its sequence word was seen; a
+// system-scope acquire would invalidate the XCD's L2 -- per request, under the
+// batch kernels sharing it), the fold, the acknowledgement, the result.  The
+// staging bytes [0, off + len) sit at the inline area's start (64-byte
+// aligned, so address parity is the staging's).
+__device__ __forceinline__ void svc_inline(const Arr &mb, uint32_t s, uint32_t sq, uint32_t lane, uint64_t t_seen) {
+  const uint32_t base = s * kSvcSlotWords;
+  const uint32_t nck = (sq >> 16) & 0xffu;
+  auto ld4 = [&](uint32_t c) {
+    const uint32_t q = base + kSvcInline + 4u * c;
+    return u32x4{ld_u32<kSys | kVolatile>(mb, q), ld_u32<kSys | kVolatile>(mb, q + 1u),
+                 ld_u32<kSys | kVolatile>(mb, q + 2u), ld_u32<kSys | kVolatile>(mb, q + 3u)};
+  };
+  const uint32_t f = lane < 16u ? ld_u32<kSys | kVolatile>(mb, base + lane) : 0u;
+  u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
+  if (lane < nck) v0 = ld4(lane);
+  if (64u + lane < nck) v1 = ld4(64u + lane);
+  auto field = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k); };
+  const uint32_t off = field(2), len = field(3);
+  uint32_t acc = range_sum(v0, (int)(16u * lane) - (int)off, 0, (int)len) +
+                 range_sum(v1, (int)(16u * (64u + lane)) - (int)off, 0, (int)len);
+  acc = group_sum<64>(acc);
+  if (lane == 0) {
+    uint64_t sum = fold16_64(acc);
+    if (!field(4) && (off & 1u)) sum = swap16((uint32_t)sum);
+    // (readlane returns int: through uint32_t, or a source address above 2^31
+    // would be sign-extended into the 64-bit sum)
+    if (field(5)) sum += (uint64_t)field(6) + field(7) + (field(8) << 8) + swap16(field(9) & 0xffffu);
+    const uint32_t res = ~fold16_64(sum) & 0xffffu;
+    const uint64_t out = (uint64_t)field(kBoxOut) | ((uint64_t)field(kBoxOut + 1) << 32);
+    st_u32<kSys>(mb, base + kBoxAck, sq);  // (read by the next launch, after this one retired)
+    scalar_result((uint32_t *)out, sq, res, field(10) != 0u, t_seen);
+  }
+}
+
 extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(const uint32_t *slab, uint32_t nslots,
                                                                              uint32_t *exitw, uint32_t token,
                                                                              uint32_t idle_ticks) {
   __shared__ uint32_t part[kScalarThreads / 64];
   __shared__ uint32_t req[16];  // [0] sequence, [1] slot, [2..10] fields, [11] a burst, [12] served by wave 0,
-                                // [13] exit, [14..15] the staging buffer's bytes / low half of its address
+                                // [13] exit, [14] the staging buffer's bytes, [15] inline requests for waves 1..7
   __shared__ uint64_t s_ptr[2];  // the slot's result block and staging buffer
   __shared__ u32x4 s_args[8];    // a burst's BurstArgs
+  __shared__ uint32_t x_slot[kScalarThreads / 64], x_seq[64];  // inline requests for waves 1..7
+  __shared__ uint64_t s_tseen;
   const Arr mb = arr_of(slab, 4ull * kSvcSlotWords * (kSvcSlots + 1));  // the slab, read at system scope
   // nslots: the slots in bits 0..7, the poll period in bits 8..15 (in units
   // of s_sleep 1, 64 clocks; 0 = 1)
   const uint32_t ns = (nslots & 0xffu) < kSvcSlots ? (nslots & 0xffu) : kSvcSlots;
   const uint32_t poll = (nslots >> 8) & 0xffu;
+  const uint32_t waves = nslots >> 16 & 1u ? 1u : kScalarThreads / 64;  // (bit 16: serve one request at a time)
   // wave 0, lane k < ns: slot k's last served sequence word (its ack word at
   // launch); lane 63: the control word at launch
   const uint32_t lane = threadIdx.x & 63u;
@@ -1666,43 +1706,49 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
         // the batch kernels sharing it)
         const uint32_t base = s * kSvcSlotWords;
         const uint32_t nck = (sq >> 16) & 0xffu;
-        u32x4 v0{0, 0, 0, 0}, v1{0, 0, 0, 0};
-        auto ld4 = [&](uint32_t c) {
-          const uint32_t q = base + kSvcInline + 4u * c;
-          return u32x4{ld_u32<kSys | kVolatile>(mb, q), ld_u32<kSys | kVolatile>(mb, q + 1u),
-                       ld_u32<kSys | kVolatile>(mb, q + 2u), ld_u32<kSys | kVolatile>(mb, q + 3u)};
-        };
-        const uint32_t f = lane < 16u ? ld_u32<kSys | kVolatile>(mb, base + lane) : 0u;
-        if (lane < nck) v0 = ld4(lane);
-        if (64u + lane < nck) v1 = ld4(64u + lane);
-        auto field = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k); };
-        const uint64_t out = (uint64_t)field(kBoxOut) | ((uint64_t)field(kBoxOut + 1) << 32);
         burst = (sq >> 30) & 1u;
-        if (burst && lane < nck && lane < 8u) s_args[lane] = v0;
         if (!burst && nck) {
-          // the inline span: its staging bytes [0, off + len) sit at the inline
-          // area's start (64-byte aligned, so address parity is the staging's)
-          const uint32_t off = field(2), len = field(3);
-          uint32_t acc = range_sum(v0, (int)(16u * lane) - (int)off, 0, (int)len) +
-                         range_sum(v1, (int)(16u * (64u + lane)) - (int)off, 0, (int)len);
-          acc = group_sum<64>(acc);
-          if (lane == 0) {
-            uint64_t sum = fold16_64(acc);
-            if (!field(4) && (off & 1u)) sum = swap16((uint32_t)sum);
-            // (readlane returns int: through uint32_t, or a source address
-            // above 2^31 would be sign-extended into the 64-bit sum)
-            if (field(5)) sum += (uint64_t)field(6) + field(7) + (field(8) << 8) + swap16(field(9) & 0xffffu);
-            const uint32_t res = ~fold16_64(sum) & 0xffffu;
-            st_u32<kSys>(mb, base + kBoxAck, sq);  // (read by the next launch, after this one retired)
-            scalar_result((uint32_t *)out, sq, res, field(10) != 0u, t_seen);
-          }
+          // an inline span: wave 0 serves it at once; up to seven more pending
+          // inline requests go to waves 1..7, in round-robin order after it
+          svc_inline(mb, s, sq, lane, t_seen);
           served = 1;
-        }
-        if (lane >= 2 && lane < 11) req[lane] = f;
-        if (lane == 0) {
-          s_ptr[0] = out;
-          s_ptr[1] = (uint64_t)field(kBoxStage) | ((uint64_t)field(kBoxStage + 1) << 32);
-          req[14] = field(kBoxStageBytes);
+          const uint64_t inl =
+              __ballot(lane < ns && lane != s && w != last && ((w >> 16) & 0xffu) != 0u && !((w >> 30) & 1u));
+          uint64_t m1 = inl & (~0ull << (s + 1u)), m2 = inl & ((2ull << s) - 1u), picked = 0;
+          uint32_t cnt = 0, lastpick = s;
+          while (cnt + 1u < waves && (m1 | m2)) {
+            uint64_t &m = m1 ? m1 : m2;
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1u;
+            picked |= 1ull << k;
+            if (lane == 0) x_slot[cnt] = k;
+            ++cnt;
+            lastpick = k;
+          }
+          if (picked >> lane & 1u) {
+            x_seq[lane] = w;
+            last = w;
+          }
+          rr = lastpick + 1u;
+          if (lane == 0) {
+            req[15] = cnt;
+            s_tseen = t_seen;
+          }
+        } else {
+          const uint32_t f = lane < 16u ? ld_u32<kSys | kVolatile>(mb, base + lane) : 0u;
+          auto field = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)f, (int)k); };
+          if (burst && lane < nck && lane < 8u) {
+            const uint32_t q = base + kSvcInline + 4u * lane;
+            s_args[lane] = u32x4{ld_u32<kSys | kVolatile>(mb, q), ld_u32<kSys | kVolatile>(mb, q + 1u),
+                                 ld_u32<kSys | kVolatile>(mb, q + 2u), ld_u32<kSys | kVolatile>(mb, q + 3u)};
+          }
+          if (lane >= 2 && lane < 11) req[lane] = f;
+          if (lane == 0) {
+            s_ptr[0] = (uint64_t)field(kBoxOut) | ((uint64_t)field(kBoxOut + 1) << 32);
+            s_ptr[1] = (uint64_t)field(kBoxStage) | ((uint64_t)field(kBoxStage + 1) << 32);
+            req[14] = field(kBoxStageBytes);
+            req[15] = 0;
+          }
         }
       }
       if (lane == 0) {
@@ -1760,6 +1806,13 @@ extern "C" __global__ __launch_bounds__(kScalarThreads) void mi_aql_dropin_svc(c
           st_u32<kSys>(ob, 7u, (uint32_t)(tc - t_seen));
         }
         scalar_result(out, sq, 0u, trace, t_seen);
+      }
+    } else if (req[12]) {
+      // waves 1..req[15]: the further inline requests wave 0 picked
+      const uint32_t wv = threadIdx.x >> 6;
+      if (wv >= 1u && wv <= req[15]) {
+        const uint32_t s2 = x_slot[wv - 1u];
+        svc_inline(mb, s2, x_seq[s2], threadIdx.x & 63u, s_tseen);
       }
     } else if (!req[12]) {
       // a staged span, every wave: the staging bytes are ordinary page-locked
@@ -3666,7 +3719,13 @@ int svc_ensure(AqlDevice *a) {
   static_assert(sizeof(SvcArgs) == 32, "kernel-argument layout of mi_aql_dropin_svc");
   const uint32_t token = g_svc_tokens.fetch_add(1u) + 1u;
   const uint32_t idle = batch_busy() ? std::min(dropin_svc_idle_ticks(), 5000u) : dropin_svc_idle_ticks();  // 50 us
-  const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8), a->svc_host_dev, token, idle};
+  // (MI_CKSUM_SVC_SERIAL=1, diagnostics: one request at a time, no parallel
+  // inline requests -- the A/B of tools/dropin_threads.c)
+  static const uint32_t serial = [] {
+    const char *e = getenv("MI_CKSUM_SVC_SERIAL");
+    return e && e[0] == '1' ? 1u << 16 : 0u;
+  }();
+  const SvcArgs s{a->slab_dev, kSvcSlots | (g_svc_poll.load() << 8) | serial, a->svc_host_dev, token, idle};
   hsa_signal_store_relaxed(a->svc_sig, 1);
   hsa_queue_t *q = dq_queue_locked(a, true);
   int rc = q ? dq_dispatch_locked(a, q, kAqlSvc, 1, kScalarThreads, &s, sizeof s, a->svc_karg, a->svc_sig) : -EIO;
