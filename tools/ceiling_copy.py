@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--frame", type=int, default=1514)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--grid", default="8192")
+    ap.add_argument("--unroll", default="4", help="comma list of 2, 4, 8")
+    ap.add_argument("--saux", default="0,1,2,3", help="comma list of store policies")
+    ap.add_argument("--geom", default="slots,dense")
+    ap.add_argument("--soff", default="0,6")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     lib = C.CDLL(os.path.join(ROOT, "tools", "libceiling.so"))
@@ -46,10 +50,12 @@ def main():
     dp = (C.c_void_p * R)(*[t.data_ptr() for t in dsts])
     alg = n * (2 * fr + 1)
     geoms = {"slots": (sstride, dstride, doff), "dense": (nch * 16, nch * 16, 0)}
-    for geom, (ss, ds_, do) in geoms.items():
-        for soff in (0, 6):
-            for saux in (0, 1, 2, 3):
-                for unroll in (4,):
+    ints = lambda x: [int(v) for v in x.split(",")]  # noqa: E731
+    for geom in a.geom.split(","):
+        ss, ds_, do = geoms[geom]
+        for soff in ints(a.soff):
+            for saux in ints(a.saux):
+                for unroll in ints(a.unroll):
                     for grid in [int(g) for g in a.grid.split(",")]:
                         args = (sp, dp, R, sbytes, dbytes, n, ss, soff, ds_, do, nch, unroll, grid)
                         lib.ceil_copy(*args, 100, 2, saux)
