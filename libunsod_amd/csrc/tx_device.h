@@ -439,6 +439,23 @@ __device__ __forceinline__ void tx_frame_generic(const TxDesc &t, __amdgpu_buffe
   if (lane == 0) st_u8(ta.status, i, tx_status(pl, l4_store));
 }
 
+// Pass p's two loads per destination chunk (tx_cut) into xa / xb, its cuts
+// into cut.
+template <int G, int U>
+__device__ __forceinline__ void tx_issue(const TxSegs &sg, uint32_t p, int lane, uint32_t h, __amdgpu_buffer_rsrc_t rs,
+                                         u32x4 (&xa)[U], u32x4 (&xb)[U], TxCut (&cut)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
+    xa[u] = ld16_src(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
+    xb[u] = ld16_src(rs, c.two && !c.slow ? c.A2 : kOOB);
+    cut[u] = c;
+  }
+}
+#ifndef MI_TX_EARLY_LOADS
+#define MI_TX_EARLY_LOADS 0
+#endif
+
 // U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
 // prefetch costs ~10 and a few spill to scratch): profiles/tx_copy_r02.jsonl,
 // socket frames 59-64 us per launch against 64-66 without the prefetch and
@@ -587,20 +604,18 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
       const uint32_t lim = t.src_bytes - 16u;  // A (u32, negatives wrap) is loadable iff A <= lim
       const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
       u32x4 held{0, 0, 0, 0};
+      u32x4 xa[U], xb[U];
+      TxCut cut[U];
+      if (npass) tx_issue<G, U>(sg, 0u, lane, h, rs, xa, xb, cut);
       for (uint32_t p = 0; p < npass; ++p) {
         u32x4 v[U];
-        u32x4 xa[U], xb[U];
-        TxCut cut[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const TxCut c = tx_cut(sg, p * (G * U) + u * G + lane, h);
-          xa[u] = ld16_src(rs, c.q0 < sg.L && !c.slow ? c.A1 : kOOB);
-          xb[u] = ld16_src(rs, c.two && !c.slow ? c.A2 : kOOB);
-          cut[u] = c;
-        }
         if (p == 0) prefetch2();
 #pragma unroll
         for (int u = 0; u < U; ++u) v[u] = tx_build(sg, cut[u], xa[u], xb[u], rs);
+        // the next pass's loads go out BEFORE this pass's stores: vmcnt counts
+        // stores too and retires in order, so loads issued after the stores
+        // could not be waited for without also waiting for the stores' acks
+        if (MI_TX_EARLY_LOADS && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
@@ -612,6 +627,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         }
         fold_all(v, 0, p);
         store_all(v, 0, nch, p, 0, (int)len, p == 0 ? 1 : 0);
+        if (!MI_TX_EARLY_LOADS && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
       }
       if (npass == 0) {
         ok = do_ip = do_l4 = false;
