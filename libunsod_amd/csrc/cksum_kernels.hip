@@ -1932,19 +1932,40 @@ hsa_status_t fault_event(const hsa_amd_event_t *ev, void *) {
   fprintf(stderr, "libmicksum: GPU memory fault at 0x%llx (reason 0x%x%s%s%s)\n", (unsigned long long)va, why,
           why & HSA_AMD_MEMORY_FAULT_PAGE_NOT_PRESENT ? " page-not-present" : "",
           why & HSA_AMD_MEMORY_FAULT_READ_ONLY ? " read-only" : "", why & HSA_AMD_MEMORY_FAULT_IMPRECISE ? " imprecise" : "");
-  const uint64_t top = g_jseq.load(std::memory_order_acquire), now_t = mono_s();
-  constexpr uint64_t kNear = 1u << 20;  // ranges within 1 MiB of the address
-  int near = 0, recent = 0;
+  // Snapshot the ring BEFORE printing: the process keeps journaling while
+  // this prints, and a slot rewritten under the reader would lend an old
+  // entry a newer entry's fields (each copy is checked against its sequence
+  // number before and after, seqlock-style).
+  struct Snap {
+    uint64_t s;
+    const char *what;
+    uint64_t p, bytes;
+    uint32_t tag;
+    double t;
+  };
+  static Snap snap[kJournal];  // (one fault report at a time: the runtime's event thread)
+  const uint64_t top = g_jseq.load(std::memory_order_acquire);
+  const double now_t = mono_s();
+  uint32_t ns = 0;
   for (uint64_t s = top; s > 0 && s + kJournal > top; --s) {
     const JEnt &e = g_journal[s % kJournal];
-    if (e.seq.load(std::memory_order_acquire) != s || !e.what) continue;
+    if (e.seq.load(std::memory_order_acquire) != s) continue;
+    Snap c{s, e.what, e.p, e.bytes, e.tag, e.t};
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (e.seq.load(std::memory_order_relaxed) != s || !c.what) continue;
+    snap[ns++] = c;
+  }
+  constexpr uint64_t kNear = 1u << 20;  // ranges within 1 MiB of the address
+  int near = 0, recent = 0;
+  for (uint32_t k = 0; k < ns; ++k) {
+    const Snap &e = snap[k];
     const bool hit = e.bytes && va + kNear >= e.p && va < e.p + e.bytes + kNear;
     const bool launch = !e.p && recent < 24;
     if (!hit && !launch) continue;
     if (hit) ++near;
     else ++recent;
     fprintf(stderr, "libmicksum:   %s#%llu %.6f s ago: %s tag %u [0x%llx, +%llu)%s\n", hit ? "near " : "     ",
-            (unsigned long long)s, now_t - e.t, e.what, e.tag, (unsigned long long)e.p, (unsigned long long)e.bytes,
+            (unsigned long long)e.s, now_t - e.t, e.what, e.tag, (unsigned long long)e.p, (unsigned long long)e.bytes,
             hit && va >= e.p && va < e.p + e.bytes ? "  <-- holds the address" : "");
   }
   fprintf(stderr, "libmicksum: %d journal ranges near the address (of the last %u events)\n", near, kJournal);
