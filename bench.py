@@ -43,6 +43,13 @@ CONFIGS = {
     "9000": (65536, 9000, 9216, 142),
     "64": (1 << 20, 46, 64, 14),
 }
+# <cfg>_split: ONE batch of CONFIGS[cfg]'s packets split into contiguous packet
+# ranges over the ranks ("N/G packets per GPU") -- strong
+# scaling; the plain uniform configs give every rank its own batch (weak).
+SPLIT = {"1500_split": "1500", "9000_split": "9000"}
+# tx: the fused TX copy + checksum over 65536 x 1500 B
+# socket-layout mbuf chains (mi_cksum_tx_copy)
+ALL_CONFIGS = list(CONFIGS) + ["pareto"] + list(SPLIT) + ["tx"]
 
 
 def parse():
@@ -54,7 +61,7 @@ def parse():
                          "(launch under torch.distributed.run --nproc-per-node 1)")
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=40)
-    ap.add_argument("--config", default="1500", choices=list(CONFIGS) + ["pareto"])
+    ap.add_argument("--config", default="1500", choices=ALL_CONFIGS)
     ap.add_argument("--rotate", type=int, default=0, help="distinct batches cycled (0: enough for >= 1 GiB)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-host-path", action="store_true")
@@ -85,13 +92,15 @@ def parse():
                          "'sustained', not part of value; 0 = off)")
     a = ap.parse_args()
     if a.also == "auto":
-        a.also = ["9000", "64", "pareto"] if a.config == "1500" else []
+        # the split legs only differ from the weak-scaled ones at N > 1
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        a.also = (["9000", "64", "pareto", "tx"] + (list(SPLIT) if world > 1 else [])) if a.config == "1500" else []
     elif a.also == "none":
         a.also = []
     else:
         a.also = [c for c in a.also.split(",") if c]
         for c in a.also:
-            if c not in list(CONFIGS) + ["pareto"]:
+            if c not in ALL_CONFIGS:
                 ap.error(f"--also {c}: unknown config")
     a.also = [c for c in a.also if c != a.config]
     return a
@@ -119,6 +128,18 @@ def build_workload(mi, synth, shard, config: str, rotate: int, offs64: bool, dev
         cfg = dict(workload=workload, packets_total=total_n, packets_this_rank=n, seed="0x9A7E70", alpha=1.16,
                    offsets="u64" if offs64 else "u32")
         stride = first = L = None
+    elif config in SPLIT:
+        n_total, L, stride, first = CONFIGS[SPLIT[config]]
+        lo, hi = shard.shard_uniform(n_total, world, rank)
+        n = hi - lo
+        lens = offs = None
+        L_sum = n * L
+        size = first + (n - 1) * stride + L + 64
+        workload = (f"one {n_total} x {L} B IPv4/TCP RX verify batch split into contiguous packet ranges over "
+                    f"{world} GPU(s) (slot stride {stride}, IP at +{first})")
+        scaling = "strong"
+        cfg = dict(workload=workload, packets_total=n_total, packets_this_rank=n, first_packet=lo,
+                   ip_datagram_len=L, slot_stride=stride, ip_offset=first)
     else:
         n, L, stride, first = CONFIGS[config]
         lens = offs = None
@@ -407,6 +428,17 @@ def main():
     if args.wait == "busy":
         mi.set_busy_wait(True)
 
+    if args.config == "tx":  # the TX leg alone (its rocprof / PMC passes)
+        row = tx_leg(mi, synth, shard, args, args.steps, dev, dist, backend, rank, world)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": row["value"], "unit": "GiB/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup, "ms_per_step": row["ms_per_step"],
+                              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+                              "data": "synthetic TX socket chains", "config": {"workload": row["workload"]},
+                              "roofline": row["roofline"], "config_tx": row}), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     wl = build_workload(mi, synth, shard, args.config, args.rotate, args.offs64, dev, rank, world, args.outputs)
     wl["name"] = args.config
     K = args.steps
@@ -452,6 +484,12 @@ def main():
     # same run, same K / W / submission, same output check, and reported
     # beside the headline with its own roofline.
     for also in args.also:
+        if also == "tx":
+            result["config_tx"] = tx_leg(mi, synth, shard, args, K, dev, dist, backend, rank, world)
+            result["timed_outputs_checked"] = result["timed_outputs_checked"] and result["config_tx"]["timed_outputs_checked"]
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            continue
         wl2 = build_workload(mi, synth, shard, also, 0, args.offs64, dev, rank, world, args.outputs)
         wl2["name"] = also
         m2 = measure(mi, shard, wl2, args, K, dev, dist, backend)
@@ -479,6 +517,115 @@ def main():
         print(json.dumps(result), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, world: int) -> dict:
+    """config_tx: the fused TX copy + checksum (mi_cksum_tx_copy; SURVEY.md 8(f)
+    rank 2: uinet_if_dpdk.c:590-606 m_copydata into the rte_mbuf + ip_output.c:
+    649-672 / in_delayed_cksum :958-983) over 65536 x 1500 B IPv4/TCP frames whose
+    chains have the socket layout tcp_output builds (a header mbuf + payload
+    pieces in 2 KiB socket-buffer clusters, synth.build_tx_chains), copied into
+    2176 B rte_mbuf slots (data at +128).  A step = one launch over one batch
+    (HIP launches alternating over two streams; the engine of the RX legs has
+    no TX entry point).  Same bracket as the RX legs: barrier + synchronize,
+    K launches, synchronize, max over ranks; outputs poisoned before and checked
+    after (every covered batch's status 0 and its slots verifying clean under the
+    RX kernel).  Weak-scaled: every rank copies its own batch."""
+    n, L, stride, dst_first, l3 = 65536, 1500, 2176, 128, 14
+    frame = L + l3
+    d = synth.build_tx_chains(n, L, layout="socket", seed=0x7E57 + rank, l3_off=l3)
+    dst_bytes = dst_first + n * stride + 64
+    per = d["src"].nbytes + dst_bytes
+    R = 1 + -(-(2 << 30) // (2 * n * frame))  # >= 2 GiB of other batches between reuses
+    src_host = torch.from_numpy(d["src"])
+    batches = []
+    for _ in range(R):
+        src = src_host.to(dev)
+        dst = torch.zeros(dst_bytes, dtype=torch.uint8, device=dev)
+        tb = mi.TxBatch(src, d["seg_off"], d["seg_len"], d["pkt_seg"], d["pkt_len"], dst, dst_stride=stride,
+                        dst_first=dst_first, room=stride - dst_first, l3_off=l3, max_len=frame)
+        batches.append((tb, torch.empty(n, dtype=torch.uint8, device=dev)))
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+
+    def run(k: int):
+        for j in range(k):
+            tb, st = batches[j % R]
+            mi.tx_copy(tb, status=st, stream=streams[j % len(streams)])
+
+    def verify_slots(tb) -> int:
+        """Frames of tb's slots that do NOT verify under the RX kernel."""
+        pb = mi.PktBatch(tb.dst, n, stride=stride, first_off=dst_first + l3, fixed_len=L)
+        r = mi.ipv4_verify(pb, bad_count=True)
+        torch.cuda.synchronize()
+        return int(r["bad"].item())
+
+    run(2)
+    torch.cuda.synchronize()
+    if verify_slots(batches[0][0]) or bool((batches[0][1] != 0).any()):
+        raise SystemExit(f"rank {rank}: TX copy output does not verify")
+    tw = time.perf_counter()
+    run(max(args.warmup, 1))
+    while time.perf_counter() - tw < args.settle:
+        run(50)
+        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for tb, st in batches:  # poison: covered batches must come back copied + summed
+        tb.dst.zero_()
+        st.fill_(0xFF)
+    torch.cuda.synchronize()
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+    ev1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gate = torch.cuda.Event()
+    gate.record(streams[0])
+    for s_ in streams[1:]:
+        s_.wait_event(gate)
+    for e, s_ in zip(ev0, streams):
+        e.record(s_)
+    run(K)
+    for e, s_ in zip(ev1, streams):
+        e.record(s_)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    span_us = max(ev0[0].elapsed_time(e) for e in ev1) * 1e3  # events on the launch streams
+    covered = min(K, R)
+    bad_frames = sum(verify_slots(batches[j][0]) for j in range(covered))
+    st_ok = all(bool((batches[j][1] == 0).all()) for j in range(covered))
+    untouched = all(bool((batches[j][1] == 0xFF).all()) for j in range(covered, R))
+    checked = bad_frames == 0 and st_ok and untouched
+    if not checked:
+        raise SystemExit(f"rank {rank}: timed TX outputs: {bad_frames} frames do not verify, status ok {st_ok}")
+    my_bytes = float(n) * L * K
+    elapsed, job_bytes, job_pkts = shard.job_totals(t1 - t0, my_bytes, float(n) * K,
+                                                    device=dev if dist and backend == "nccl" else None)
+    alg = float(n) * (2 * frame + 1)  # frame read + frame written + 1 B status
+    us = span_us / K
+    roof = dict(bound="hbm", achieved=round(alg / us / 1e3, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(alg / us / 1e3 / HBM_PEAK_GBS, 4), traffic=None, kernel="k_tx_copy (mi_cksum_tx_copy)",
+                alg_bytes_per_launch=int(alg), avg_launch_us=round(us, 2), streams=len(streams),
+                wall_frac=round(alg * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))
+    tf = os.path.join(ROOT, "profiles", "r06", "pmc_traffic_r06.json")
+    try:
+        ent = json.load(open(tf)).get("tx") if os.path.exists(tf) else None
+    except Exception:
+        ent = None
+    if ent:
+        roof["traffic"] = ent["bytes_per_launch"]
+        roof["traffic_source"] = "profiles/r06/pmc_traffic_r06.json[tx] (rocprofv3 --pmc, separate passes; not this run)"
+    return dict(value=round(job_bytes / elapsed / GIB, 2), unit="GiB/s", ms_per_step=round(elapsed / K * 1e3, 5),
+                mpkt_per_s=round(job_pkts / elapsed / 1e6, 2), scaling="weak",
+                frames_copied_gibs=round(job_pkts * frame / elapsed / GIB, 2),
+                workload=(f"{n} x {frame} B frames (IPv4/TCP, {L} B datagrams), socket-layout mbuf chains "
+                          f"({round(len(d['seg_len']) / n, 2)} mbufs per frame) -> 2176 B rte_mbuf slots, "
+                          "copy + ip_sum + th_sum fused; value = IP datagram bytes checksummed"),
+                rotating_batches=R, footprint_MiB=round(R * per / 2**20, 1), roofline=roof,
+                timed_outputs_checked=checked, frames_checked=covered * n,
+                submit=f"HIP launches over {len(streams)} streams", kernel_env=os.environ.get("MI_CKSUM_TX_KERNEL", "lanes"))
 
 
 def _oracle_layout(lay: dict) -> dict:
@@ -565,13 +712,14 @@ def plumbing_64k(seconds: float = 1.0) -> dict:
 
 def dropin_latency(mi, calls: int = 400) -> dict:
     """(b1) drop-in cost per call on this host: libmicksum's in_cksum_hdr /
-    in_cksum_pseudo_header / in_cksum_skip (the bytes read over PCIe from
-    pinned staging; one AQL dispatch per call, and through the device's
-    resident drop-in service -- ``gpu_dropin_us`` is the library's default
-    mode) against the reference's own functions (oracle/_ref) on the same real
-    mbuf chains.  Median over `calls` calls through ctypes; ``ctypes_floor_us``
-    is the same loop around in_addword (no checksum work) and is included in
-    every figure."""
+    in_cksum_pseudo_header / in_cksum_skip on real mbuf chains -- in the
+    library's default mode (``dropin_us``: MI_DROPIN_HOST, the host fold on the
+    calling core) and in its GPU mode (the bytes read over PCIe from pinned
+    staging; one AQL dispatch per call, and through the device's resident
+    drop-in service) -- against the reference's own functions (oracle/_ref) on
+    the same chains.  Median over `calls` calls through ctypes;
+    ``ctypes_floor_us`` is the same loop around in_addword (no checksum work)
+    and is included in every figure."""
     import ctypes as C
     from oracle.pyoracle import Oracle, available
     lib = mi.load()
@@ -616,29 +764,33 @@ def dropin_latency(mi, calls: int = 400) -> dict:
                                                    C.c_uint8]
     lib.mi__set_dropin_service.restype = C.c_int
     lib.mi__set_dropin_service.argtypes = [C.c_int]
-    default_mode = lib.mi__set_dropin_service(0)  # (returns the setting it replaces)
-    lib.mi__set_dropin_service(default_mode)
-    out["default_mode"] = "service" if default_mode else "dispatch"
-
-    def both(g, args):
-        # one AQL dispatch per call, and the device's resident drop-in service
-        r = {}
-        for mode, on in (("dispatch", 0), ("service", 1)):
-            lib.mi__set_dropin_service(on)
-            r[mode] = med(g, args)
-        lib.mi__set_dropin_service(default_mode)
-        return r
+    svc_default = lib.mi__set_dropin_service(0)  # (returns the setting it replaces)
+    lib.mi__set_dropin_service(svc_default)
+    mode_default = mi.set_dropin_mode("host")
+    mi.set_dropin_mode(mode_default)
+    out["default_mode"] = mode_default + ("" if mode_default == "host" else
+                                          " (service)" if svc_default else " (dispatch)")
+    degraded0 = mi.dropin_degraded()
 
     for name, (fn, args) in cases.items():
         g = getattr(lib, fn)
-        modes = both(g, args)
-        row = dict(gpu_dropin_us=modes[out["default_mode"]], gpu_dispatch_us=modes["dispatch"],
-                   gpu_service_us=modes["service"])
+        mi.set_dropin_mode("host")
+        row = dict(dropin_us=None, host_fold_us=med(g, args))
+        want = int(g(*args))
+        mi.set_dropin_mode("gpu")
+        for mode, on in (("dispatch", 0), ("service", 1)):
+            lib.mi__set_dropin_service(on)
+            row[f"gpu_{mode}_us"] = med(g, args)
+            assert int(g(*args)) == want, f"{fn}: GPU drop-in ({mode}) differs from the host fold"
+        lib.mi__set_dropin_service(svc_default)
+        mi.set_dropin_mode(mode_default)
+        row["dropin_us"] = med(g, args)
         if ref is not None:
             r = getattr(ref, "ref_" + fn)
-            assert int(g(*args)) == int(r(*args)), f"{fn}: drop-in differs from the reference"
+            assert want == int(r(*args)), f"{fn}: drop-in differs from the reference"
             row["reference_cpu_us"] = med(r, args)
         out[name] = row
+    out["gpu_calls_degraded_to_host"] = mi.dropin_degraded() - degraded0
     return out
 
 

@@ -9,19 +9,18 @@
  *
  *  (b1) drop-in scalar entry points with the reference's exact names and
  *       signatures -- they replace the MACHINE_SRCS object in_cksum.o inside
- *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  Each call
- *       gathers the mbuf chain into a per-thread pinned staging buffer and
- *       posts it to the device's drop-in service -- one resident workgroup
- *       for all threads, polling a mailbox slot per thread in VRAM the host
- *       writes through the PCIe BAR (spans up to 2 KiB travel in the slot
- *       itself) -- then spins on a pinned result word: in_cksum_hdr ~2.7-3.3
- *       us, a 1480-byte in_cksum_pseudo_header ~3.3-4.0 us per call on the
- *       MI355X host (MI_CKSUM_DROPIN_MAILBOX=host: slots in
- *       page-locked host memory, ~5 us; MI_CKSUM_DROPIN_SERVICE=0: one AQL
- *       dispatch per call, ~8 us).  This
- *       level is the compatibility path (the reference's call sites unchanged);
- *       per-packet RX/TX throughput comes from (b2) at the burst / inject-ring
- *       batch points.
+ *       libuinet (src/lib/libuinet/Makefile:275-276) at link time.  They are
+ *       scalar and synchronous (~0.13 us for an IPv4 header on one core), so
+ *       by default they are served on the calling CPU (MI_DROPIN_HOST: the
+ *       chain is folded in place by host_fold.c, no GPU, no allocation, no
+ *       error) -- SURVEY.md 8(b1): "per-call GPU dispatch is not viable".
+ *       MI_DROPIN_GPU (mi_cksum_set_dropin_mode, or MI_CKSUM_DROPIN=gpu in the
+ *       environment) sends each call to the device's resident drop-in service
+ *       instead -- one workgroup for all threads polling a mailbox slot per
+ *       thread in VRAM the host writes through the PCIe BAR -- 2.7-3.3 us per
+ *       in_cksum_hdr.  This level is the compatibility path;
+ *       per-packet RX/TX throughput comes from (b2) at the burst /
+ *       inject-ring batch points.
  *
  *  (b2) batch offload: a batch of packets that already sits in device memory
  *       (the RX burst / TX inject-ring batch points, uinet_if_dpdk.c:854-879 and
@@ -29,9 +28,8 @@
  *
  * Results are bit-identical to the reference on the same bytes at the same
  * addresses (address parity matters only for in_cksum_hdr, in_cksum.c:278-285).
- * There is no CPU fallback: without a usable gfx950 device the batch calls
- * return -ENODEV and the (b1) calls abort with a message (or, with
- * mi_cksum_set_dropin_error_handler, report and return 0xffff).
+ * The batch calls (b2) have no CPU fallback: without a usable gfx950 device
+ * they return -ENODEV.  The (b1) calls need no device in their default mode.
  */
 #ifndef MI_CKSUM_H
 #define MI_CKSUM_H
@@ -74,18 +72,27 @@ unsigned short in_pseudo(unsigned int a, unsigned int b, unsigned int c);
 /* in_cksum.c:172-179 -- one's-complement add of two u16. */
 unsigned short in_addword(unsigned short a, unsigned short b);
 
+/* (b1) serving mode, process-wide:
+ *   MI_DROPIN_HOST (default) -- folded on the calling CPU, in place over the
+ *     chain (libunsod_amd/csrc/host_fold.c); never fails, needs no device;
+ *   MI_DROPIN_GPU -- through the device's resident drop-in service (or one
+ *     AQL dispatch per call with MI_CKSUM_DROPIN_SERVICE=0).
+ * The environment's MI_CKSUM_DROPIN=gpu|host sets the initial mode.  Returns
+ * the previous mode, or -EINVAL. */
+#define MI_DROPIN_HOST 0
+#define MI_DROPIN_GPU 1
+int mi_cksum_set_dropin_mode(int mode);
+
 /* (b1) error policy.  The reference's functions cannot fail and return only
- * the sum, so a drop-in whose GPU dispatch fails (no device, a queue error, no
- * result within 10 s) prints the error and aborts by default: any value it
- * returned would be a wrong checksum.  A handler installed here is called
- * instead with the function name and mi_cksum_strerror(), and the call
- * returns 0xffff.  No datagram with valid sums verifies to 0xffff (valid ones
- * verify to 0; ~fold(S) is 0xffff only for all-zero bytes), so an RX caller
- * (ip_input.c:463-469, tcp_input.c:716-720) drops the packet.  On TX the
- * value is stored into the outgoing header like any other result.  NULL
- * restores the default.  Process-wide. */
+ * the sum.  In MI_DROPIN_GPU mode a call whose GPU request fails (no device,
+ * a queue error, no result within 10 s) is served by the host fold instead --
+ * the same bits -- and counted (mi_cksum_dropin_degraded); a handler installed
+ * here is told first, with the function name and mi_cksum_strerror().  NULL
+ * removes it.  Nothing aborts.  Process-wide. */
 typedef void (*mi_cksum_error_fn)(const char *what, const char *err);
 void mi_cksum_set_dropin_error_handler(mi_cksum_error_fn fn);
+/* GPU-mode drop-in calls an error sent to the host fold, since start. */
+uint64_t mi_cksum_dropin_degraded(void);
 
 /* ------------------------------------------------------------------------ */
 /* runtime                                                                    */
@@ -511,7 +518,12 @@ int mi_cksum_rx_offload_host(const mi_pkt_batch *b, uint32_t *csum_flags, uint32
                              uint32_t *bad_count);
 
 /* Page-lock and map / unlock a host range for mi_cksum_ipv4_verify_host
- * (hipHostRegister, mapped + portable). */
+ * (hipHostRegister, mapped + portable).  The runtime locks whole pages, so
+ * a range may not share a page with another registered range (-EEXIST);
+ * unregister takes the exact pointer that was registered (-ENOENT
+ * otherwise) and must come before the memory is freed.  Register memory the
+ * caller owns page by page -- DPDK hugepages, an mmap -- not a sub-range of a
+ * malloc heap block. */
 int mi_cksum_host_register(void *p, uint64_t bytes);
 int mi_cksum_host_unregister(void *p);
 

@@ -165,7 +165,11 @@ SIGNATURES = {
     "mi_cksum_synth_ipv4": (C.c_int, [C.POINTER(PktBatchC), C.c_uint64, C.c_void_p]),
     "mi_cksum_hsa_queues": (C.c_int, []),
     "mi_cksum_set_dropin_error_handler": (None, [C.c_void_p]),
+    "mi_cksum_set_dropin_mode": (C.c_int, [C.c_int]),
+    "mi_cksum_dropin_degraded": (C.c_uint64, []),
 }
+# (b1) serving modes (include/mi_cksum.h)
+MI_DROPIN_HOST, MI_DROPIN_GPU = 0, 1
 
 # mi_cksum_error_fn: void (*)(const char *what, const char *err)
 DROPIN_ERROR_FN = C.CFUNCTYPE(None, C.c_char_p, C.c_char_p)

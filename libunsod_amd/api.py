@@ -502,7 +502,35 @@ def rx_offload_host(buf: np.ndarray, n: int, *, offs=None, stride: int = 0, firs
 
 
 def host_register(buf: np.ndarray) -> None:
+    """mi_cksum_host_register.  Register memory owned page by page (e.g.
+    ``page_buffer``), never a view into a malloc heap block that Python may
+    free and reuse while the pages are locked."""
     check("mi_cksum_host_register", load().mi_cksum_host_register(buf.ctypes.data, buf.nbytes))
+
+
+def page_buffer(nbytes: int) -> np.ndarray:
+    """A uint8 array of ``nbytes`` on pages of its own: an anonymous mmap,
+    page-aligned, that no other object shares and that malloc never hands
+    out again -- what host_register should be given (the role DPDK's
+    hugepage memory plays for the reference's mbufs)."""
+    import mmap
+    m = mmap.mmap(-1, max(1, (nbytes + 4095) & ~4095))
+    return np.frombuffer(m, np.uint8, count=nbytes)
+
+
+def set_dropin_mode(mode: str) -> str:
+    """Serve the (b1) drop-ins on the CPU ("host", the default) or through the
+    device's drop-in service ("gpu"); returns the previous mode."""
+    from ._lib import MI_DROPIN_GPU, MI_DROPIN_HOST
+    names = {MI_DROPIN_HOST: "host", MI_DROPIN_GPU: "gpu"}
+    was = load().mi_cksum_set_dropin_mode({"host": MI_DROPIN_HOST, "gpu": MI_DROPIN_GPU}[mode])
+    check("mi_cksum_set_dropin_mode", min(was, 0))
+    return names[was]
+
+
+def dropin_degraded() -> int:
+    """GPU-mode drop-in calls that an error sent to the host fold."""
+    return int(load().mi_cksum_dropin_degraded())
 
 
 def host_unregister(buf: np.ndarray) -> None:

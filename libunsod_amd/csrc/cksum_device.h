@@ -201,16 +201,25 @@ __device__ __noinline__ void arr_oob(const char *fn, int line, uint32_t off, uin
 // to (the host-shared mailbox and result words); bit 31 volatile (a poll the
 // compiler must not hoist).
 constexpr int kSys = 1 | 16, kVolatile = (int)(1u << 31);
+// Byte offset of element i of SZ-byte elements, or kOOB when it does not fit
+// 32 bits: a corrupt index (a descriptor's segment number of 2^29 and up)
+// must read the out-of-range zero, not wrap to another, valid, entry.
+template <uint32_t SZ>
+__device__ __forceinline__ uint32_t elem_off(uint32_t i) {
+  return i < kOOB / SZ ? SZ * i : kOOB;
+}
 template <int AUX = 0>
 __device__ __forceinline__ uint32_t ld_u32(const Arr &a, uint32_t i MI_AT) {
-  ARR_CHECK(a, 4u * i, 4u);
-  return __builtin_amdgcn_raw_buffer_load_b32(a.r, 4u * i, 0, AUX);
+  const uint32_t o = elem_off<4>(i);
+  ARR_CHECK(a, o, 4u);
+  return __builtin_amdgcn_raw_buffer_load_b32(a.r, o, 0, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ uint64_t ld_u64(const Arr &a, uint32_t i MI_AT) {
-  ARR_CHECK(a, 8u * i, 8u);
+  const uint32_t o = elem_off<8>(i);
+  ARR_CHECK(a, o, 8u);
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(a.r, 8u * i, 0, AUX);
+  const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(a.r, o, 0, AUX);
   return (uint64_t)v.x | ((uint64_t)v.y << 32);
 }
 __device__ __forceinline__ uint32_t ld_u8(const Arr &a, uint32_t i MI_AT) {
@@ -219,19 +228,22 @@ __device__ __forceinline__ uint32_t ld_u8(const Arr &a, uint32_t i MI_AT) {
 }
 template <int AUX = 0>
 __device__ __forceinline__ void st_u32(const Arr &a, uint32_t i, uint32_t v MI_AT) {
-  ARR_CHECK(a, 4u * i, 4u);
-  __builtin_amdgcn_raw_buffer_store_b32(v, a.r, 4u * i, 0, AUX);
+  const uint32_t o = elem_off<4>(i);
+  ARR_CHECK(a, o, 4u);
+  __builtin_amdgcn_raw_buffer_store_b32(v, a.r, o, 0, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ void st_u64(const Arr &a, uint32_t i, uint64_t v MI_AT) {
-  ARR_CHECK(a, 8u * i, 8u);
+  const uint32_t o = elem_off<8>(i);
+  ARR_CHECK(a, o, 8u);
   typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, a.r, 8u * i, 0, AUX);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)v, (uint32_t)(v >> 32)}, a.r, o, 0, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ void st_u16(const Arr &a, uint32_t i, uint32_t v MI_AT) {
-  ARR_CHECK(a, 2u * i, 2u);
-  __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, a.r, 2u * i, 0, AUX);
+  const uint32_t o = elem_off<2>(i);
+  ARR_CHECK(a, o, 2u);
+  __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, a.r, o, 0, AUX);
 }
 template <int AUX = 0>
 __device__ __forceinline__ void st_u8(const Arr &a, uint32_t i, uint32_t v MI_AT) {
@@ -239,8 +251,9 @@ __device__ __forceinline__ void st_u8(const Arr &a, uint32_t i, uint32_t v MI_AT
   __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, a.r, i, 0, AUX);
 }
 __device__ __forceinline__ void add_u32(const Arr &a, uint32_t i, uint32_t v MI_AT) {
-  ARR_CHECK(a, 4u * i, 4u);
-  (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)v, a.r, (int)(4u * i), 0, 0);
+  const uint32_t o = elem_off<4>(i);
+  ARR_CHECK(a, o, 4u);
+  (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)v, a.r, (int)o, 0, 0);
 }
 
 // A wave-uniform struct of dwords at byte `off` of an array (the multi-batch

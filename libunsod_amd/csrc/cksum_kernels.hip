@@ -2474,7 +2474,9 @@ bool deal_plan(const Desc &d, Shape sh, F fn_of, const void **fn, unsigned *bloc
   if (!*fn) return false;
   const unsigned res = resident_blocks(*fn);
   const uint64_t units = ((uint64_t)d.n + 64u / sh.g - 1) / (64u / sh.g);
-  if (!res || units <= 4ull * res) return false;
+  // counter c serves the workgroups b % kDealCtrs == c: a grid smaller than
+  // the counter set would leave the slices of counters gridDim.x.. undealt
+  if (res < kDealCtrs || units <= 4ull * res) return false;
   *blocks = res;
   return true;
 }
@@ -4706,13 +4708,36 @@ int mi_cksum_synth_ipv4(const mi_pkt_batch *b, uint64_t seed, void *stream) {
 // one of them (a read past a mapping would fault the GPU).
 // Each keeps the GPU address of its registered pointer, found once at
 // registration, instead of a hipHostGetDevicePointer (a runtime lookup) per
-// call.
+// call.  Ranges never share a page (a registration overlapping a registered
+// page is refused) and an unregistration names its range by the exact pointer
+// it was registered with: round 5's table matched the first range whose pages
+// held the pointer, so unregistering the second of two ranges that shared a
+// page erased the FIRST one's entry and left the unmapped range's entry --
+// and its cached GPU address -- live for any later host batch that malloc
+// placed in those pages.
 struct HostRange {
   uintptr_t lo, hi;  // whole pages
   uintptr_t p, dev;  // the registered pointer and its GPU address
 };
 static std::mutex g_reg_mu;
 static std::vector<HostRange> g_reg;
+
+static void reg_pages(const void *p, uint64_t bytes, uintptr_t *lo, uintptr_t *hi) {
+  *lo = (uintptr_t)p & ~(uintptr_t)4095;
+  *hi = ((uintptr_t)p + bytes + 4095) & ~(uintptr_t)4095;
+}
+// g_reg_mu held: the entry whose pages overlap [lo, hi), or -1.
+static long reg_overlap(uintptr_t lo, uintptr_t hi) {
+  for (size_t k = 0; k < g_reg.size(); ++k)
+    if (lo < g_reg[k].hi && hi > g_reg[k].lo) return (long)k;
+  return -1;
+}
+// g_reg_mu held: the entry registered at exactly p, or -1.
+static long reg_exact(const void *p) {
+  for (size_t k = 0; k < g_reg.size(); ++k)
+    if (g_reg[k].p == (uintptr_t)p) return (long)k;
+  return -1;
+}
 
 // The GPU address of host bytes [p, p + bytes) (rounded up to 16), or nullptr
 // when they do not lie inside one registered range.
@@ -4725,37 +4750,73 @@ static void *host_dev_ptr(const void *p, uint64_t bytes) {
 }
 
 int mi_cksum_host_register(void *p, uint64_t bytes) {
+  if (!p || !bytes) return set_err(-EINVAL, "mi_cksum_host_register: empty range");
   int rc = ensure_ctx();
   if (rc) return rc;
+  uintptr_t lo, hi;
+  reg_pages(p, bytes, &lo, &hi);
+  // held across the runtime calls: two threads registering overlapping
+  // ranges at once must not both pass the check
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  const long k = reg_overlap(lo, hi);
+  if (k >= 0)
+    return set_err(-EEXIST, "mi_cksum_host_register: [%p, +%llu) shares a page with the range registered at %p",
+                   p, (unsigned long long)bytes, (void *)g_reg[(size_t)k].p);
   HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped | hipHostRegisterPortable));
   jnote("host register", p, bytes);
+  jnote("host register pages", (const void *)lo, hi - lo);
   dbg_mem("host-register", p, bytes);
   void *dev = nullptr;
   if (hipHostGetDevicePointer(&dev, p, 0) != hipSuccess || !dev) {
     (void)hipHostUnregister(p);
     return set_err(-EIO, "mi_cksum_host_register: no device address for the range");
   }
-  // the mapping covers whole pages
-  const uintptr_t lo = (uintptr_t)p & ~(uintptr_t)4095, hi = ((uintptr_t)p + bytes + 4095) & ~(uintptr_t)4095;
-  std::lock_guard<std::mutex> g(g_reg_mu);
   g_reg.push_back({lo, hi, (uintptr_t)p, (uintptr_t)dev});
   return 0;
 }
 
 int mi_cksum_host_unregister(void *p) {
+  uintptr_t lo = 0, hi = 0;
   {
     std::lock_guard<std::mutex> g(g_reg_mu);
-    const uintptr_t a = (uintptr_t)p;
-    for (size_t k = 0; k < g_reg.size(); ++k)
-      if (a >= g_reg[k].lo && a < g_reg[k].hi) {
-        g_reg.erase(g_reg.begin() + (long)k);
-        break;
-      }
+    const long k = reg_exact(p);
+    if (k < 0) return set_err(-ENOENT, "mi_cksum_host_unregister: %p was not registered", p);
+    lo = g_reg[(size_t)k].lo;
+    hi = g_reg[(size_t)k].hi;
+    g_reg.erase(g_reg.begin() + k);
   }
   dbg_mem("host-unregister", p, 0);
-  jnote("host unregister", p, alloc_bytes(p));
+  jnote("host unregister pages", (const void *)lo, hi - lo);
   HIP_TRY(hipHostUnregister(p));
   return 0;
+}
+
+// The table alone, without the runtime (tests/test_abi.py checks the
+// bookkeeping on the CPU): insert a range with a made-up GPU address (0 or
+// -EEXIST), remove by exact pointer (0 or -ENOENT), look a span up (its GPU
+// address or 0), count, clear.
+extern "C" int mi__reg_table_insert(void *p, uint64_t bytes, uint64_t dev) {
+  if (!p || !bytes) return -EINVAL;
+  uintptr_t lo, hi;
+  reg_pages(p, bytes, &lo, &hi);
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  if (reg_overlap(lo, hi) >= 0) return -EEXIST;
+  g_reg.push_back({lo, hi, (uintptr_t)p, (uintptr_t)dev});
+  return 0;
+}
+extern "C" int mi__reg_table_remove(void *p) {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  const long k = reg_exact(p);
+  if (k < 0) return -ENOENT;
+  g_reg.erase(g_reg.begin() + k);
+  return 0;
+}
+extern "C" uint64_t mi__reg_table_lookup(const void *p, uint64_t bytes) {
+  return (uint64_t)(uintptr_t)host_dev_ptr(p, bytes);
+}
+extern "C" int mi__reg_table_count(void) {
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  return (int)g_reg.size();
 }
 
 // The service machinery shared by the (b1) drop-ins (mi__scalar_fold) and the
@@ -5600,11 +5661,5 @@ int mi__dropin_service_owners(void) {
 // Where the calling thread's service slot lives: 0 none yet, 1 page-locked
 // host memory, 2 device memory written through the BAR.  (tests, bench)
 int mi__dropin_mailbox(void) { return t_aql1.slot < 0 ? 0 : t_aql1.dev->slab_vram ? 2 : 1; }
-
-void mi__fatal(const char *what) {
-  fprintf(stderr, "libmicksum: %s: %s\n", what, t_err[0] ? t_err : "unknown error");
-  fflush(stderr);
-  abort();
-}
 
 }  // extern "C"

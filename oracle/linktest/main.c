@@ -6,8 +6,13 @@
  * reference.  Prints one JSON line; exit status 0 iff every value matches.
  */
 #include <stdio.h>
+#include <stdlib.h>
 
 extern int mi_link_kats(void);
+/* libmicksum's own symbols (include/mi_cksum.h): which mode served the
+ * drop-ins, and how many GPU-mode calls an error sent to the host fold. */
+extern int mi_cksum_set_dropin_mode(int mode);
+extern unsigned long long mi_cksum_dropin_degraded(void);
 extern unsigned int mi_link_got[];
 
 static const struct {
@@ -47,6 +52,11 @@ main(void)
 		printf("%s\"%s\": [\"0x%04x\", \"0x%04x\", %s]", i ? ", " : "", kat[i].name, mi_link_got[i],
 		       kat[i].want, ok ? "true" : "false");
 	}
-	printf("}, \"failed\": %d}\n", bad);
+	{
+		int mode = mi_cksum_set_dropin_mode(0);
+		mi_cksum_set_dropin_mode(mode);
+		printf("}, \"failed\": %d, \"mode\": \"%s\", \"degraded\": %llu}\n", bad,
+		       mode == 1 ? "gpu" : "host", mi_cksum_dropin_degraded());
+	}
 	return bad ? 1 : 0;
 }

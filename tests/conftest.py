@@ -60,17 +60,39 @@ def aligned(a: np.ndarray, align: int = 64):
     return raw, v
 
 
-@pytest.fixture(params=["dispatch", "service"])
+@pytest.fixture(params=["host", "dispatch", "service"])
 def dropin_mode(request):
-    """The (b1) drop-ins as one AQL dispatch per call, or through the thread's
-    resident drop-in service (MI_CKSUM_DROPIN_SERVICE); restored afterwards."""
+    """The (b1) drop-ins on the CPU (MI_DROPIN_HOST, the default), as one AQL
+    dispatch per call, or through the device's resident drop-in service
+    (MI_DROPIN_GPU; MI_CKSUM_DROPIN_SERVICE); restored afterwards.  In the GPU
+    modes no call may have been served by the host fold (a GPU error degrades
+    to it): the results checked came from the GPU."""
     import ctypes as C
 
+    import libunsod_amd as mi
     from libunsod_amd._lib import load
     lib = load()
     lib.mi__set_dropin_service.restype = C.c_int
     lib.mi__set_dropin_service.argtypes = [C.c_int]
+    gpu = request.param != "host"
+    mode_was = mi.set_dropin_mode("gpu" if gpu else "host")
     was = lib.mi__set_dropin_service(1 if request.param == "service" else 0)
     assert was in (0, 1)
+    degraded = mi.dropin_degraded()
     yield request.param
     assert lib.mi__set_dropin_service(was) in (0, 1)
+    mi.set_dropin_mode(mode_was)
+    if gpu:
+        assert mi.dropin_degraded() == degraded, "a GPU-mode drop-in was served by the host fold"
+
+
+@pytest.fixture
+def gpu_dropins():
+    """The (b1) drop-ins through the GPU (MI_DROPIN_GPU) for one test, and no
+    call served by the host fold."""
+    import libunsod_amd as mi
+    was = mi.set_dropin_mode("gpu")
+    degraded = mi.dropin_degraded()
+    yield
+    mi.set_dropin_mode(was)
+    assert mi.dropin_degraded() == degraded, "a GPU-mode drop-in was served by the host fold"

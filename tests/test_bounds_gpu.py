@@ -28,6 +28,14 @@ from libunsod_amd import synth
 from libunsod_amd._lib import ChainBatchC, LIB_DIR, MI_CHAIN_SKIP, check, load
 from oracle.pyoracle import Oracle
 
+
+@pytest.fixture(autouse=True)
+def _gpu_mode(gpu_dropins):
+    """These tests are about the GPU drop-in path (MI_DROPIN_GPU); the host
+    fold, the default, is tests/test_dropin_host.py."""
+    yield
+
+
 pytestmark = pytest.mark.gpu
 ORC = Oracle("port")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

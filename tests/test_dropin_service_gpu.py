@@ -22,6 +22,14 @@ from libunsod_amd import synth
 from libunsod_amd._lib import load
 from oracle.pyoracle import Oracle
 
+
+@pytest.fixture(autouse=True)
+def _gpu_mode(gpu_dropins):
+    """These tests are about the GPU drop-in path (MI_DROPIN_GPU); the host
+    fold, the default, is tests/test_dropin_host.py."""
+    yield
+
+
 pytestmark = pytest.mark.gpu
 ORC = Oracle("port")
 
@@ -96,10 +104,9 @@ def test_service_runs_beside_host_burst(lib):
     first-use costs outlast the service's 1 ms idle exit.)"""
     n, L, stride, first = 200, 1500, 2176, 142
     b = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=3)
-    raw = np.zeros(b["buf"].size + 4096, np.uint8)
-    s = (-raw.ctypes.data) % 4096
-    buf = raw[s:s + b["buf"].size]
+    buf = mi.page_buffer(b["buf"].size)  # registrable: pages of its own
     buf[:] = b["buf"]
+    raw = buf
     ORC.ipv4_finalize_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
     buf[first + 5 * stride + 99] ^= 0x11
     want = ORC.ipv4_verify_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
@@ -216,9 +223,9 @@ def test_small_host_bursts_through_the_service(lib, demux_golden):
     options, fragments, bad sums, malformed headers) in bursts of 1-128 must
     give the golden ip / l4 / status and the same RX offload flags as one
     720-datagram launch, with u64 and u32 offsets."""
-    from conftest import aligned
     g = demux_golden
-    keep, buf = aligned(g["ver_in"].copy(), 4096)
+    buf = mi.page_buffer(g["ver_in"].size)  # registrable: pages of its own
+    buf[:] = g["ver_in"]
     offs, flen = g["offs"].astype(np.int64), g["flen"].astype(np.int32)
     n = len(offs)
     mi.host_register(buf)

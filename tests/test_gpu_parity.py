@@ -252,7 +252,8 @@ def test_host_zero_copy(layout):
         b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=16)
         lay = dict(offs=offs, lens=lens)
         olay = fin = dict(offs=offs, flen=lens.astype(np.uint32))
-    keep, host = aligned(b0["buf"], 4096)
+    host = mi.page_buffer(b0["buf"].size)  # registrable: pages of its own
+    host[:] = b0["buf"]
     ORC.ipv4_finalize_batch(host, n, **fin)
     rng = np.random.default_rng(3)
     host[rng.choice(host.size, 25, replace=False)] ^= 0x40
@@ -452,7 +453,9 @@ def _rx_mix(n, seed):
     hl = np.minimum(hl, (lens // 4) * 4)
     offs = synth.packed_offsets(lens + 8, first_off=2)
     b0 = synth.build_ipv4_batch(n, lens, offs=offs, proto=proto, hl=hl, seed=seed, payload="random")
-    keep, h = aligned(b0["buf"])
+    h = mi.page_buffer(b0["buf"].size)  # registrable (test_host_paths_offsets): pages of its own
+    h[:] = b0["buf"]
+    keep = h
     o = offs.astype(np.int64)
     frag = rng.random(n) < 0.05
     for i in np.nonzero(frag)[0]:

@@ -45,10 +45,10 @@ def test_rx_offload_host_bursts(n):
     """rte_eth_rx_burst-sized bursts (<= 512, dpdk_helper.h:20; ring of 4096,
     uinet_api.c:1983) in 2176 B rte_mbuf slots, registered and staged."""
     from libunsod_amd import synth
-    from conftest import aligned
     stride, first, L = 2176, 142, 1500
     b0 = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=n)
-    keep, h = aligned(b0["buf"], 4096)
+    h = mi.page_buffer(b0["buf"].size)  # registrable: pages of its own
+    h[:] = b0["buf"]
     ORC.ipv4_finalize_batch(h, n, stride=stride, first_off=first, fixed_flen=L)
     h[first + (n // 2) * stride + 700] ^= 4
     want = ORC.ipv4_verify_batch(h, n, stride=stride, first_off=first, fixed_flen=L)

@@ -31,11 +31,17 @@ def test_kernel_side_object_needs_only_the_abi():
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(BIN), reason="linktest not built (needs /root/reference at build time)")
-def test_linked_kernel_caller_kats():
-    p = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+@pytest.mark.parametrize("mode", ["host", "gpu"])
+def test_linked_kernel_caller_kats(mode):
+    """All 28 SURVEY.md 8(a) known answers through the kernel-side caller, served
+    by the host fold (the default) and by the GPU drop-in service -- in GPU mode
+    none of them by the host fold after a GPU error (degraded == 0)."""
+    p = subprocess.run([BIN], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, MI_CKSUM_DROPIN=mode))
     assert p.returncode == 0, p.stdout + p.stderr
     res = json.loads(p.stdout)
     assert res["failed"] == 0 and res["kats"] == 28
+    assert res["mode"] == mode and res["degraded"] == 0
 
 
 OFFLOAD_BIN = os.path.join(ROOT, "oracle", "_ref", "offload_test")

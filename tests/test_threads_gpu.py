@@ -26,6 +26,14 @@ from libunsod_amd import synth
 from libunsod_amd._lib import load
 from oracle.pyoracle import Oracle
 
+
+@pytest.fixture(autouse=True)
+def _gpu_mode(gpu_dropins):
+    """These tests are about the GPU drop-in path (MI_DROPIN_GPU); the host
+    fold, the default, is tests/test_dropin_host.py."""
+    yield
+
+
 pytestmark = pytest.mark.gpu
 ORC = Oracle("port")
 
@@ -45,10 +53,9 @@ def kfd_queues():
 def _burst(seed):
     n, L, stride, first = 64, 1500, 2176, 142
     b = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=seed)
-    raw = np.zeros(b["buf"].size + 4096, np.uint8)
-    s = (-raw.ctypes.data) % 4096
-    buf = raw[s:s + b["buf"].size]
+    buf = mi.page_buffer(b["buf"].size)  # registrable: pages of its own
     buf[:] = b["buf"]
+    raw = buf
     ORC.ipv4_finalize_batch(buf, n, stride=stride, first_off=first, fixed_flen=L)
     return raw, buf, n, stride, first, L
 

@@ -82,10 +82,8 @@ def test_tx_full_size_then_rx_verify():
 
 def _host_buf(a: np.ndarray) -> np.ndarray:
     """a copy of ``a`` in a 4 KiB-aligned, whole-page numpy buffer (registrable)."""
-    raw = np.zeros(a.size + 3 * 4096, np.uint8)
-    s = (-raw.ctypes.data) % 4096
     n = (a.size + 4095) & ~4095
-    out = raw[s:s + n]
+    out = mi.page_buffer(n)  # registrable: pages of its own
     out[:a.size] = a
     return out
 
