@@ -351,7 +351,10 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 // RG (byte-balanced ranges, VERDICT r4 "do this" 3, experiment): wave w
 // takes datagrams [starts[w], starts[w+1]) -- at most 64, cut so each range
 // holds about the same bytes -- instead of the 64 at 64 w; one range per wave.
-template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false>
+// PIPE (round 6, VERDICT r5 "do this" 4): the next pass's loads are issued
+// before this pass is scanned, so a wave streaming a long range keeps a pass
+// in flight while it scans (one more register set).
+template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false, bool PIPE = false>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes,
                                             const uint32_t *starts = nullptr, uint32_t nr = 0,
@@ -467,6 +470,14 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
 #endif
       uint32_t carry = 0, qs = 0, qe = 0;
       for (uint32_t cb = 0;;) {
+        u32x4 vn[PIPE ? U : 1];
+        if constexpr (PIPE) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t c = cb + W + 64u * u + lane;
+            vn[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+          }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const uint32_t x = sum4(v[u]);  // chunks past the run load as zeros
@@ -494,8 +505,12 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
         if (cb >= nch) break;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const uint32_t c = cb + 64u * u + lane;
-          v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+          if constexpr (PIPE) {
+            v[u] = vn[u];
+          } else {
+            const uint32_t c = cb + 64u * u + lane;
+            v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
+          }
         }
         __builtin_amdgcn_wave_barrier();  // lookups done before the next pass rewrites s_q
       }
@@ -564,11 +579,11 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
 #ifndef MI_RUN_MINW
 #define MI_RUN_MINW 1  // waves per SIMD the flat-run kernel is held to (register budget experiments)
 #endif
-template <int U, int MODE = 0, int NW = kBlock / 64>
+template <int U, int MODE = 0, int NW = kBlock / 64, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out,
                                                                 uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
                                                                 uint32_t abs_lanes) {
-  packed_body<U, MODE, NW>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+  packed_body<U, MODE, NW, false, PIPE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
 template <int U, int NW>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_ranges(Desc d, uint16_t *ip_out, uint16_t *l4_out,
@@ -1435,6 +1450,14 @@ MI_AQL_RUN_W(4, 1)
 MI_AQL_RUN_W(4, 2)
 MI_AQL_RUN_W(8, 1)
 MI_AQL_RUN_W(8, 2)
+// (the same, pipelined passes: mi_aql_run<U>w2p)
+#define MI_AQL_RUN_WP(U_)                                                                               \
+  extern "C" __global__ __launch_bounds__(128) void mi_aql_run##U_##w2p(                                \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
+    packed_body<U_, 0, 2, false, true>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                             \
+  }
+MI_AQL_RUN_WP(4)
+MI_AQL_RUN_WP(8)
 #define MI_AQL_RUN(U_)                                                                                  \
   extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
                                                            uint32_t *bad) {                             \
@@ -2315,6 +2338,7 @@ struct Plan {
   int run_u;    // kPlanRun: chunks per lane per pass
   int run_nw = 4;  // kPlanRun: waves per workgroup (k_ipv4_verify_packed<U, 0, NW>)
   int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
+  bool pipe = false;  // kPlanRun, 2 waves: the pipelined passes (packed_body PIPE)
 };
 
 // The LDS-DMA flat run (k_ipv4_verify_run_dma) for packed batches with offset
@@ -2342,6 +2366,17 @@ int run_dma_code() {
   return c;
 }
 
+// Pipelined passes of the 2-wave flat run (MI_CKSUM_RUN_PIPE=1; mi__set_run_pipe).
+std::atomic<int> g_run_pipe{-1};
+bool run_pipe() {
+  int v = g_run_pipe.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_RUN_PIPE");
+    v = e && e[0] == '1' ? 1 : 0;
+    g_run_pipe.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
 // Waves per workgroup of the flat-run verify (MI_CKSUM_RUN_WAVES = 1, 2 or 4;
 // mi__set_run_waves for tests).  2 by default: on the 2^22 Pareto batch 2-wave
 // workgroups ran 196.8-197.5 us against 203.1-203.5 (4 waves) and 201.8-202.5
@@ -2379,6 +2414,7 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
   if (((d.flags & MI_BATCH_PACKED) || dense_slots) && !g_tune.g) {
     Plan pl{kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
     pl.run_nw = pl.run_u == 16 ? 4 : run_waves();
+    pl.pipe = pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_pipe();
     // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
     // offset / length arrays: batches whose arrays reach kOOB take the register
     // kernel, whose descriptor reads are 64-bit)
@@ -2523,6 +2559,14 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     VLAUNCH((k_ipv4_verify_packed<U_, 0, NW_>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);         \
     return launched();                                                                                       \
   }
+    if (pl.pipe && pl.run_nw == 2 && pl.run_u == 4) {
+      VLAUNCH((k_ipv4_verify_packed<4, 0, 2, true>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      return launched();
+    }
+    if (pl.pipe && pl.run_nw == 2 && pl.run_u == 8) {
+      VLAUNCH((k_ipv4_verify_packed<8, 0, 2, true>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      return launched();
+    }
     X(4, 1) X(4, 2) X(8, 1) X(8, 2)
 #undef X
   }
@@ -2660,7 +2704,14 @@ Shape pick_tx_shape(uint32_t max_len) {
 // can switch.
 int tx_kernel_kind() {
   const char *e = getenv("MI_CKSUM_TX_KERNEL");
-  return e && !strcmp(e, "wave") ? 2 : 0;
+  return e && !strcmp(e, "wave") ? 2 : e && !strcmp(e, "lds") ? 3 : 0;
+}
+// The 8x2 lane-group kernel with the next pass's loads issued before this
+// pass's stores (k_tx_copy EL): MI_CKSUM_TX_EARLY=1 / 0, read
+// per call (A/B in one process); unset: the build default MI_TX_EARLY_LOADS.
+bool tx_early_loads() {
+  const char *e = getenv("MI_CKSUM_TX_EARLY");
+  return e ? e[0] == '1' : MI_TX_EARLY_LOADS != 0;
 }
 
 int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
@@ -2678,7 +2729,31 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
     hipLaunchKernelGGL((k_tx_wave<2>), dim3(grid_for(t.n, 64)), dim3(kBlock), 0, s, t);
     return launched();
   }
+  if (tx_kernel_kind() == 3) {
+    // the LDS-staged gather: one wave (8 frames) per workgroup, the same total
+    // waves as k_tx_copy's grid
+    const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)t.n + 7u) / 8u, 4ull * grid_for(t.n, 8));
+    // MI_CKSUM_TX_LDS = "UxR": chunks per lane per pass, ring depth (read per
+    // call: A/B in one process); default 2 x MI_TX_LDS_R
+    int u = 2, r = MI_TX_LDS_R;
+    if (const char *e = getenv("MI_CKSUM_TX_LDS")) (void)sscanf(e, "%dx%d", &u, &r);
+#define X(U_, R_)                                                                         \
+  if (u == U_ && r == R_) {                                                               \
+    hipLaunchKernelGGL((k_tx_lds<U_, R_>), dim3(grid ? grid : 1u), dim3(64), 0, s, t);    \
+    return launched();                                                                    \
+  }
+    X(2, 2) X(2, 3) X(2, 4) X(1, 4)
+#undef X
+    return set_err(-EINVAL, "no LDS TX kernel %dx%d", u, r);
+  }
   const int grid = grid_for(t.n, sh.g);
+  if (sh.g == 8 && sh.u == 2) {
+    if (tx_early_loads())
+      hipLaunchKernelGGL((k_tx_copy<8, 2, true>), dim3(grid), dim3(kBlock), 0, s, t);
+    else
+      hipLaunchKernelGGL((k_tx_copy<8, 2, false>), dim3(grid), dim3(kBlock), 0, s, t);
+    return launched();
+  }
 #define X(G_, U_)                                                                  \
   if (sh.g == G_ && sh.u == U_) {                                                  \
     hipLaunchKernelGGL((k_tx_copy<G_, U_>), dim3(grid), dim3(kBlock), 0, s, t);    \
@@ -2708,7 +2783,7 @@ enum AqlKernelId {
 #define X(G_, U_) kAqlVD_##G_##x##U_,
   MI_DEAL_SHAPES(X)
 #undef X
-  kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2,
+  kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2, kAqlRun4w2p, kAqlRun8w2p,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2722,6 +2797,7 @@ const char *const kAqlNames[kAqlKernels] = {
     MI_DEAL_SHAPES(X)
 #undef X
     "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
+    "mi_aql_run4w2p", "mi_aql_run8w2p",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2735,6 +2811,7 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #undef X
     (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
     (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
+    (const void *)mi_aql_run4w2p, (const void *)mi_aql_run8w2p,
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3061,6 +3138,7 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks, b
   }
   if (pl.kind == kPlanRun) {
     if (pl.run_nw == 1) *id = pl.run_u == 4 ? kAqlRun4w1 : kAqlRun8w1;
+    else if (pl.run_nw == 2 && pl.pipe) *id = pl.run_u == 4 ? kAqlRun4w2p : kAqlRun8w2p;
     else if (pl.run_nw == 2) *id = pl.run_u == 4 ? kAqlRun4w2 : kAqlRun8w2;
     else *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
     *blocks = run_blocks(d, pl.run_nw);
@@ -3176,7 +3254,7 @@ void aql_fill_raw(uint8_t *ka, const void *args, uint32_t nargs, unsigned blocks
 unsigned aql_wg(int id) {
   switch (id) {
     case kAqlRun4w1: case kAqlRun8w1: return 64;
-    case kAqlRun4w2: case kAqlRun8w2: return 128;
+    case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: return 128;
     case kAqlScalar: return kScalarThreads;
     default: return kBlock;
   }
@@ -3901,6 +3979,12 @@ int mi__fault_reporter(void) { return g_fault_handler.load(); }
 unsigned long long mi__journal_events(void) { return (unsigned long long)g_jseq.load(); }
 // Diagnostics / tests (not in the public header): waves per workgroup of the
 // flat-run verify kernel (1, 2, 4; speed only, never results).
+// Pipelined flat-run passes on (1) / off (0); returns the previous setting.
+int mi__set_run_pipe(int on) {
+  const int was = run_pipe() ? 1 : 0;
+  g_run_pipe.store(on ? 1 : 0);
+  return was;
+}
 int mi__set_run_waves(int w) {
   if (w != 1 && w != 2 && w != 4) return set_err(-EINVAL, "run waves %d", w);
   g_run_waves.store(w);
@@ -4129,7 +4213,10 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
   if (pl.kind == kPlanRun && pl.dma)
     snprintf(buf, sizeof buf, "k_ipv4_verify_run_dma<%d,%d>", pl.dma / 10, pl.dma % 10);
   else if (pl.kind == kPlanRun)
-    snprintf(buf, sizeof buf, pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>" : "k_ipv4_verify_packed<%d,%d waves>",
+    snprintf(buf, sizeof buf,
+             pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>"
+             : pl.pipe      ? "k_ipv4_verify_packed<%d,%d waves,pipelined>"
+                            : "k_ipv4_verify_packed<%d,%d waves>",
              pl.run_u, pl.run_nw);
   else if (pl.kind == kPlanShape)
     snprintf(buf, sizeof buf, "k_ipv4_verify<%d,%d>", pl.shape.g, pl.shape.u);

@@ -460,7 +460,7 @@ __device__ __forceinline__ void tx_issue(const TxSegs &sg, uint32_t p, int lane,
 // prefetch costs ~10 and a few spill to scratch): profiles/tx_copy_r02.jsonl,
 // socket frames 59-64 us per launch against 64-66 without the prefetch and
 // 69 with it at 3 waves per SIMD.
-template <int G, int U>
+template <int G, int U, bool EL = MI_TX_EARLY_LOADS>
 __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) {
   static_assert(G >= 8, "the header window needs lanes 0..6 of the group");
   __shared__ uint32_t s_seg[kBlock / G][kTxSeg][2];
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         // the next pass's loads go out BEFORE this pass's stores: vmcnt counts
         // stores too and retires in order, so loads issued after the stores
         // could not be waited for without also waiting for the stores' acks
-        if (MI_TX_EARLY_LOADS && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
+        if (EL && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
         if (p == 0) {
           decide1(v[0], h + l3);
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
@@ -627,7 +627,7 @@ __global__ __launch_bounds__(kBlock, (U <= 2 ? 4 : 1)) void k_tx_copy(TxDesc t) 
         }
         fold_all(v, 0, p);
         store_all(v, 0, nch, p, 0, (int)len, p == 0 ? 1 : 0);
-        if (!MI_TX_EARLY_LOADS && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
+        if (!EL && p + 1 < npass) tx_issue<G, U>(sg, p + 1, lane, h, rs, xa, xb, cut);
       }
       if (npass == 0) {
         ok = do_ip = do_l4 = false;
@@ -977,6 +977,247 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
     }
     prefetch2();
     if (!done) tx_frame_generic<64, 1>(t, rs, rd, f, (int)lane, len, k0, k1, ip_mlen);
+  }
+}
+
+// TX fused copy, round 6: the lane-group gather of k_tx_copy with its data
+// staged through LDS (k_tx_lds, MI_CKSUM_TX_KERNEL=lds).
+//
+// k_tx_copy loads a pass's source chunks into VGPRs, so a wave holds one or
+// two passes in flight and interleaves each pass's loads with the previous
+// pass's stores.  The slot-copy probes say what the memory side wants instead
+// (tools/ceiling_copy.py, profiles/r05/ceiling_copy_r05.jsonl): a lane that
+// issues all its loads and then all its stores reaches 0.667 of 8 TB/s, one
+// that alternates over 2-8 load/store rounds 0.56-0.62.  Here the same two
+// loads per destination chunk (tx_cut: the segment holding the chunk's first
+// byte at A1, the next one at A2 when the chunk straddles a boundary) go to
+// LDS by `buffer_load_dwordx4 ... lds` -- gfx950 takes any byte address there
+// too (tools/lds_dma_probe.hip, profiles/r06/lds_dma_probe_r06.txt) -- into a
+// ring of R pass slots per wave, so R passes (R * 64 U * 16 B per wave) are in
+// flight with no VGPR held for them and a 1514 B frame's loads go out at most
+// two rounds apart from its stores.  A pass is built from its slot (tx_build),
+// folded and stored exactly as in k_tx_copy; the slot is refilled with the
+// pass R ahead once its reads have returned.
+//
+// Ordering (MI355X_MICROARCH.md, LDS-DMA): only the issuing wave's vmcnt
+// orders a ds_read behind a DMA.  Pass p's 2U DMAs are followed by the 2U of
+// each of the R-1 passes issued after them, so vmcnt <= 2U(R-1) retires them
+// (stores and descriptor loads in between only add to the count: waiting for
+// 2U(R-1) is conservative).  The ring's reads are inline asm (the compiler
+// would put a vmcnt(0) in front of a plain LDS read while a DMA is pending).
+// One wave per workgroup: the ring is the wave's own.
+#ifndef MI_TX_LDS_R
+#define MI_TX_LDS_R 3
+#endif
+template <int U>
+__device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 (&xa)[U], u32x4 (&xb)[U]) {
+  static_assert(U == 1 || U == 2, "ring reads for U = 1, 2");
+  if constexpr (U == 1) {
+    asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(xa[0]), "=&v"(xb[0])
+                 : "v"(lds_addr(slot + lane)), "v"(lds_addr(slot + 64 + lane))
+                 : "memory");
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(xa[0]), "=&v"(xb[0]), "=&v"(xa[1]), "=&v"(xb[1])
+        : "v"(lds_addr(slot + lane)), "v"(lds_addr(slot + 64 + lane)), "v"(lds_addr(slot + 128 + lane)),
+          "v"(lds_addr(slot + 192 + lane))
+        : "memory");
+  }
+}
+
+template <int U, int R>
+__global__ __launch_bounds__(64) void k_tx_lds(TxDesc t) {
+  constexpr int G = 8;
+  constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
+  static_assert(R >= 2 && R <= 4, "ring depth");
+  __shared__ uint32_t s_seg[NG][kTxSeg][2];
+  __shared__ u32x4 s_ring[R][2 * U][64];  // pass slot q % R: chunk u's A1 loads, then its A2 loads
+  typedef __attribute__((address_space(3))) void *lds_ptr;
+  Desc ds{}, dd{};
+  ds.base = t.src;
+  ds.bytes = t.src_bytes;
+  dd.base = t.dst;
+  dd.bytes = t.dst_bytes;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(ds), rd = rsrc_of(dd);
+  const TxArrs ta = tx_arrs(t);
+  const int lane = threadIdx.x & (G - 1);
+  const uint32_t grp = threadIdx.x / G;
+  const uint32_t stride = gridDim.x * NG;
+  uint32_t i = blockIdx.x * NG + grp;
+  uint32_t len_c = 0, k0_c = 0, k1_c = 0;
+  int32_t sl_c = 0;
+  uint32_t so_c = 0;
+  if (i < t.n) {
+    len_c = ld_u32(ta.pkt_len, i);
+    k0_c = ld_u32(ta.pkt_seg, i);
+    k1_c = ld_u32(ta.pkt_seg, i + 1);
+    if (k0_c + lane < k1_c) {
+      sl_c = (int32_t)ld_u32(ta.seg_len, k0_c + lane);
+      so_c = (uint32_t)ld_u64(ta.seg_off, k0_c + lane);
+    }
+  }
+  for (; i < t.n; i += stride) {
+    const uint32_t len = len_c;
+    const uint32_t k0 = k0_c, k1 = k1_c;
+    const int32_t sl0 = sl_c;
+    const uint32_t so0 = so_c;
+    const uint32_t in = i + stride;
+    uint32_t len_n = 0, k0_n = 0, k1_n = 0;
+    if (in < t.n) {
+      len_n = ld_u32(ta.pkt_len, in);
+      k0_n = ld_u32(ta.pkt_seg, in);
+      k1_n = ld_u32(ta.pkt_seg, in + 1);
+    }
+    bool pre2 = false;
+    auto prefetch2 = [&]() {
+      if (pre2) return;
+      pre2 = true;
+      sl_c = 0;
+      so_c = 0;
+      if (in < t.n && k0_n + lane < k1_n) {
+        sl_c = (int32_t)ld_u32(ta.seg_len, k0_n + lane);
+        so_c = (uint32_t)ld_u64(ta.seg_off, k0_n + lane);
+      }
+      len_c = len_n;
+      k0_c = k0_n;
+      k1_c = k1_n;
+    };
+    const uint32_t l3 = t.l3;
+    const uint32_t D = (uint32_t)(t.dst_first + (uint64_t)i * t.dst_stride);  // host-checked < 4 GiB
+    const uint32_t h = D & 15u, c0 = D & ~15u;
+    uint32_t st = len > t.room ? MI_TX_NOBUFS : 0u;
+    // walk 1 (as k_tx_copy): bytes in the chain, the IP mbuf's m_len from the
+    // IP header on, the first kTxSeg nonempty segments into LDS
+    uint32_t total = 0, ip_mlen = 0, m = 0;
+    for (uint32_t w = k0; w < k1 && !st; w += G) {
+      const uint32_t k = w + lane;
+      const uint32_t l = k < k1 ? (uint32_t)max(w == k0 ? sl0 : (int32_t)ld_u32(ta.seg_len, k), 0) : 0u;
+      const uint32_t inc = group_scan<G>(l);
+      const uint32_t a = total + inc - l, e = total + inc;
+      const uint32_t nz = l ? 1u : 0u;
+      const uint32_t zi = group_scan<G>(nz);
+      const uint32_t idx = m + zi - nz;
+      if (nz && idx < (uint32_t)kTxSeg) {
+        s_seg[grp][idx][0] = a;
+        s_seg[grp][idx][1] = (w == k0 ? so0 : (uint32_t)ld_u64(ta.seg_off, k)) - a;
+      }
+      const bool isip = l && a <= l3 && l3 < e;
+      ip_mlen += group_sum<G>(isip ? e - l3 : 0u);  // leader only
+      total += group_lane<G>(inc, G - 1);
+      m += group_lane<G>(zi, G - 1);
+    }
+    if (!st && total < len) st = MI_TX_SHORT;
+    if (st) {
+      if (lane == 0) st_u8(ta.status, i, st);
+      prefetch2();
+      continue;
+    }
+    ip_mlen = group_lane<G>(ip_mlen, 0);
+    const bool odd = (h + l3) & 1u;
+    IpHdr ih{};
+    bool ok = false, do_ip = false, do_l4 = false, udp = false, done = false;
+    uint32_t at = 0;
+    int hend = 0, lend = 0;
+    uint32_t acc_t = 0, acc_h = 0, acc_f = 0;
+    if (m <= (uint32_t)kTxSeg) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      static_assert(kTxSeg == 4, "segment registers S1..S3 / D0..D3");
+      auto seg_start = [&](uint32_t e) { return e < m ? min((int)s_seg[grp][e][0], (int)len) : (int)len; };
+      auto seg_delta = [&](uint32_t e) { return e < m ? s_seg[grp][e][1] : 0u; };
+      const uint32_t nch = (h + len + 15u) >> 4;
+      const uint32_t npass = (nch + G * U - 1) / (G * U);
+      const int S1 = seg_start(1), S2 = seg_start(2), S3 = seg_start(3);
+      const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
+      const uint32_t lim = t.src_bytes - 16u;
+      const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
+      // pass q's 2U DMAs into ring slot q % R (lanes past their frame's last
+      // pass, and loads a chunk does not need, read nothing: offset kOOB)
+      auto issue = [&](uint32_t q) {
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q % (uint32_t)R));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const TxCut c = tx_cut(sg, q * (G * U) + u * G + lane, h);
+          const bool live = q < npass && !c.slow;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)&s_ring[sl][2 * u][0], 16,
+                                                  live && c.q0 < sg.L ? c.A1 : kOOB, 0, 0, MI_TX_LOAD_AUX);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)&s_ring[sl][2 * u + 1][0], 16,
+                                                  live && c.two ? c.A2 : kOOB, 0, 0, MI_TX_LOAD_AUX);
+        }
+      };
+      u32x4 held{0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < R; ++q) issue((uint32_t)q);
+      for (uint32_t p = 0; p < npass; ++p) {
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * U * (R - 1)));  // pass p has landed
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(p % (uint32_t)R));
+        u32x4 xa[U], xb[U], v[U];
+        tx_ring_read<U>(&s_ring[sl][0][0], (int)threadIdx.x & 63, xa, xb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
+        issue(p + R);  // the slot's reads have returned (lgkmcnt(0) in tx_ring_read)
+        if (p == 0) {
+          prefetch2();
+          const u32x4 hv[1] = {v[0]};
+          ih = parse_ipv4<G, 1>(hv, h + l3);
+          const TxPlan pl = tx_plan(t, i, len, ih);
+          ok = pl.ok;
+          do_ip = pl.do_ip;
+          do_l4 = pl.do_l4;
+          udp = pl.udp;
+          at = pl.at;
+          hend = pl.hend;
+          lend = pl.lend;
+          const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+          const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+          const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
+          if ((uint64_t)need + h > 16ull * G) break;  // a sum field beyond the held chunks: generic path
+          done = true;
+          held = v[0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const uint32_t ci = p * (G * U) + u * G + lane;
+          const int rel = (int)(16u * ci) - (int)(h + l3);
+          fold_chunk(v[u], rel, lend, hend, hend > 20, acc_t, acc_h, acc_f);
+          const int cs = (int)(16u * ci) - (int)h;
+          if (ci < nch && !(p == 0 && u == 0)) store_chunk(rd, c0 + 16u * ci, v[u], -cs, (int)len - cs);
+        }
+      }
+      if (npass == 0) {
+        ok = do_ip = do_l4 = false;
+        done = true;
+      }
+      if (done) {
+        const bool l4_store = do_l4 && (uint64_t)at + 2u <= ip_mlen;
+        uint32_t c_ip, c_l4;
+        tx_sums<G>(acc_t, acc_h, acc_f, hend, ih, odd, udp, c_ip, c_l4);
+        const uint32_t pip = l3 + 10u, pl4 = l3 + at;
+        const int b0 = (int)h - (int)(16u * lane);
+        if (do_ip) {
+          if (pip < len) put_byte(held, (int)pip + b0, c_ip);
+          if (pip + 1u < len) put_byte(held, (int)pip + 1 + b0, c_ip >> 8);
+        }
+        if (l4_store) {
+          if (pl4 < len) put_byte(held, (int)pl4 + b0, c_l4);
+          if (pl4 + 1u < len) put_byte(held, (int)pl4 + 1 + b0, c_l4 >> 8);
+        }
+        const uint32_t ci = lane;
+        const int cs = (int)(16u * ci) - (int)h;
+        if (ci < nch) store_chunk(rd, c0 + 16u * ci, held, -cs, (int)len - cs);
+        if (lane == 0) st_u8(ta.status, i, (ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
+      }
+      // the ring's over-issued passes (offset kOOB: zeros) land before the
+      // next frame writes the ring or s_seg
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      __builtin_amdgcn_wave_barrier();
+    }
+    prefetch2();
+    if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
   }
 }
 

@@ -189,7 +189,8 @@ def test_process_exit_with_live_service():
             "print('ok')\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for _ in range(3):
-        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root)
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root,
+                           env=dict(os.environ, MI_CKSUM_DROPIN="gpu"))
         assert r.returncode == 0 and r.stdout.strip() == "ok", (r.returncode, r.stderr[-2000:])
     x = torch.arange(1 << 20, device="cuda", dtype=torch.int64)
     assert int(x.sum().item()) == (1 << 20) * ((1 << 20) - 1) // 2
@@ -321,7 +322,8 @@ print(json.dumps(dict(batch=[lib.mi__repeat_queue_id(rep._h, i) for i in (0, 1)]
 rep.close()
 """
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=root,
+                       env=dict(os.environ, MI_CKSUM_DROPIN="gpu"))
     assert r.returncode == 0, r.stderr[-2000:]
     import json
     got = json.loads(r.stdout.strip().splitlines()[-1])

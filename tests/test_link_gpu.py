@@ -203,7 +203,7 @@ def _frame_byte(c, i, q):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.path.exists(TX_BIN), reason="tx_test not built (needs /root/reference at build time)")
-@pytest.mark.parametrize("kernel", ["pair", "wave"])
+@pytest.mark.parametrize("kernel", ["pair", "wave", "lds"])
 def test_tx_offload_matches_reference_software_route(tmp_path, kernel):
     """VERDICT r3 "do this" 1: every tests/tx_cases.py case goes out twice
     through real struct mbufs of the reference's definition -- if_hwassist = 0

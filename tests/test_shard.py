@@ -106,3 +106,50 @@ def test_gloo_world2_byte_shards():
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=5) is True
+
+
+def _rank_uniform(rank, world, port, q):
+    """The uniform configs' strong split (bench.py 1500_split / 9000_split):
+    one batch of fixed slots, contiguous packet ranges of N/G packets."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, L, stride, first = 3001, 1500, 2176, 142
+        full = synth.build_ipv4_batch(n, L, stride=stride, first_off=first, seed=91)
+        orc = Oracle("port")
+        _, whole = aligned(full["buf"])
+        orc.ipv4_finalize_batch(whole, n, stride=stride, first_off=first, fixed_flen=L)
+        bad = np.arange(3, n, 211)
+        whole[first + bad * stride + 700] ^= 0x08
+        lo, hi = shard.shard_uniform(n, world, rank)
+        # this rank's range in a buffer of its own, same slot geometry
+        _, mine = aligned(whole[lo * stride:hi * stride + first + L].copy())
+        ip, l4, st = orc.ipv4_verify_batch(mine, hi - lo, stride=stride, first_off=first, fixed_flen=L)
+        elapsed, nbytes, npkts = shard.job_totals(0.001 * (rank + 1), float(L * (hi - lo)), float(hi - lo))
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (lo, hi, ip, l4, st))
+        if rank == 0:
+            ip_w, l4_w, st_w = orc.ipv4_verify_batch(whole, n, stride=stride, first_off=first, fixed_flen=L)
+            ok = (np.array_equal(np.concatenate([g[2] for g in gathered]), ip_w)
+                  and np.array_equal(np.concatenate([g[3] for g in gathered]), l4_w)
+                  and np.array_equal(np.concatenate([g[4] for g in gathered]), st_w)
+                  and int((st_w != 0).sum()) == len(bad) and nbytes == float(L * n) and npkts == n
+                  and elapsed == pytest.approx(0.001 * world)
+                  and [g[:2] for g in gathered] == [shard.shard_uniform(n, world, k) for k in range(world)])
+            q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_uniform_split():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_uniform, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=5) is True

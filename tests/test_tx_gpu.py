@@ -117,9 +117,10 @@ def test_tx_copy_host_matches_oracle(mode):
         assert np.array_equal(dst[c["dst"].size:], np.zeros(dst.size - c["dst"].size, np.uint8)), name
 
 
-@pytest.mark.parametrize("kernel", ["wave"])
+@pytest.mark.parametrize("kernel", ["wave", "lds"])
 def test_tx_kernel_every_case(kernel, monkeypatch):
-    """The wave-per-frame TX kernel (k_tx_wave, MI_CKSUM_TX_KERNEL=wave) on every
+    """The wave-per-frame TX kernel (k_tx_wave, MI_CKSUM_TX_KERNEL=wave) and the
+    LDS-staged gather (k_tx_lds, MI_CKSUM_TX_KERNEL=lds) on every
     edge case (socket / single / random / 40-segment chains, padding, far
     headers, short / nobufs / malformed frames, flags and data, UDP 0 ->
     0xffff), byte for byte against the oracle."""
@@ -132,7 +133,7 @@ def test_tx_kernel_every_case(kernel, monkeypatch):
         assert bad.size == 0, (kernel, name, bad.size, bad[:8])
 
 
-@pytest.mark.parametrize("kernel", ["wave"])
+@pytest.mark.parametrize("kernel", ["wave", "lds"])
 def test_tx_kernel_full_size(kernel, monkeypatch):
     monkeypatch.setenv("MI_CKSUM_TX_KERNEL", kernel)
     for layout in ("socket", "single"):

@@ -24,6 +24,8 @@ CONFIGS = {
     "9000": ("9000", "k_ipv4_verify<8, 12>", 65536 * 9000 + 5 * 65536),
     "64": ("64", "k_ipv4_verify_slot64", (1 << 20) * 46 + 5 * (1 << 20)),
     "pareto": ("pareto_u32", "k_ipv4_verify_packed<8, 0, 2>", None),
+    # bench.py config_tx: 65536 frames of 1514 B read + written + 1 B status
+    "tx": ("tx", "k_tx_copy<8, 2>", 65536 * (2 * 1514 + 1)),
 }
 
 
@@ -39,7 +41,7 @@ def medians(path: str, prefix: str) -> tuple[dict, int]:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--round", default="r05")
+    ap.add_argument("--round", default="r06")
     ap.add_argument("--pareto-alg", type=int, default=1205618850,
                     help="Pareto algorithmic bytes per launch (bench.py's alg_bytes_per_launch)")
     a = ap.parse_args()
