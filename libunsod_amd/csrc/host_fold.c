@@ -10,8 +10,9 @@
  * Shape.  The reference sums each span in ABSOLUTE-address lanes with aligned
  * loads and a masked head (in_cksumdata, in_cksum.c:91-170), then byte-swaps
  * a span whose stream offset and address disagree in parity (:222-225).  Here
- * a span is summed in lanes counted from its own first byte, with unaligned
- * 32-bit loads (one widening add per 4 bytes, which the compiler vectorizes),
+ * a span is summed in lanes counted from its own first byte -- long spans
+ * 64 bytes per step, each 32-bit word's two 16-bit halves added to 32-bit
+ * vector lane sums (four ALU ops per 32 bytes), short ones word by word --
  * and swapped when its STREAM offset is odd.  Both give the stream-relative
  * sum S of SURVEY.md 8(a)'s contract, because 2^16 == 1 (mod 65535): a
  * little-endian 32-bit word is congruent to the sum of its two 16-bit lanes,
@@ -23,67 +24,37 @@
 #include <stdint.h>
 #include <string.h>
 
-#include "mi_internal.h"
+#include "host_fold.h"
 
-/* 64 -> 16 bits, end-around carry: congruent mod 65535, 0 only if s == 0. */
-uint32_t mi__host_fold64(uint64_t s)
-{
-	s = (s & 0xffffffffu) + (s >> 32);
-	s = (s & 0xffffffffu) + (s >> 32);
-	s = (s & 0xffffu) + (s >> 16);
-	s = (s & 0xffffu) + (s >> 16);
-	s = (s & 0xffffu) + (s >> 16);
-	return (uint32_t)s;
-}
+/* The body of a long span, 64 bytes per step: every 32-bit lane is split
+ * into its two 16-bit halves, each added to a 32-bit lane sum.  A lane sum
+ * grows by at most 0xffff per step, so the sums are emptied into a 64-bit
+ * total every 32768 steps (2 MiB).  Vector extensions, not intrinsics: the
+ * AVX2 clone uses 256-bit registers, the default one 128-bit pairs. */
+typedef uint32_t v8u __attribute__((vector_size(32)));
 
-static uint32_t swap16(uint32_t f)
-{
-	return ((f & 0xffu) << 8) | (f >> 8);
-}
-
-/* The body: little-endian 32-bit words from p, widened into 64-bit sums.
- * Four independent sums so the scalar clone is not one long dependency chain;
- * 2^32 words per sum before it could carry out, far beyond any span. */
 __attribute__((target_clones("avx2", "default")))
-static uint64_t words_sum(const uint8_t *p, size_t nw)
+uint64_t mi__host_blocks_sum(const uint8_t *p, size_t nb)
 {
-	uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-	size_t i = 0;
+	uint64_t total = 0;
 
-	for (; i + 4 <= nw; i += 4) {
-		uint32_t w[4];
-		memcpy(w, p + 4 * i, 16);
-		a0 += w[0];
-		a1 += w[1];
-		a2 += w[2];
-		a3 += w[3];
+	while (nb) {
+		const size_t k = nb < 32768 ? nb : 32768;
+		v8u a0 = {0}, b0 = {0}, a1 = {0}, b1 = {0};
+		for (size_t i = 0; i < k; ++i, p += 64) {
+			v8u x, y;
+			memcpy(&x, p, 32);
+			memcpy(&y, p + 32, 32);
+			a0 += x & 0xffffu;
+			b0 += x >> 16;
+			a1 += y & 0xffffu;
+			b1 += y >> 16;
+		}
+		for (int j = 0; j < 8; ++j)
+			total += (uint64_t)a0[j] + b0[j] + a1[j] + b1[j];
+		nb -= k;
 	}
-	for (; i < nw; ++i) {
-		uint32_t w;
-		memcpy(&w, p + 4 * i, 4);
-		a0 += w;
-	}
-	return a0 + a1 + a2 + a3;
-}
-
-uint32_t mi__host_span_sum(const void *buf, size_t n)
-{
-	const uint8_t *p = (const uint8_t *)buf;
-	uint64_t s = words_sum(p, n / 4);
-	size_t i = n & ~(size_t)3;
-
-	if (n - i >= 2) {
-		s += (uint32_t)p[i] | ((uint32_t)p[i + 1] << 8);
-		i += 2;
-	}
-	if (i < n) /* an odd last byte sits in an even lane of the span: low byte */
-		s += p[i];
-	return mi__host_fold64(s);
-}
-
-uint32_t mi__host_fold_acc(uint32_t acc, uint32_t span_sum, uint64_t stream_off)
-{
-	return mi__host_fold64((uint64_t)acc + ((stream_off & 1) ? swap16(span_sum) : span_sum));
+	return total;
 }
 
 uint16_t mi__host_cksum_hdr(const void *ip)
@@ -91,9 +62,11 @@ uint16_t mi__host_cksum_hdr(const void *ip)
 	/* in_cksum.c:278-285 sums the 20 bytes in absolute-address lanes with no
 	 * odd-address correction: at an odd address that is the swapped span sum
 	 * (0xb861 where in_cksum_skip gives 0x61b8). */
-	uint32_t f = mi__host_span_sum(ip, 20);
+	uint32_t w[5], f;
 
+	memcpy(w, ip, 20);
+	f = hf_fold64((uint64_t)w[0] + w[1] + w[2] + w[3] + w[4]);
 	if ((uintptr_t)ip & 1)
-		f = swap16(f);
+		f = hf_swap16(f);
 	return (uint16_t)~f;
 }

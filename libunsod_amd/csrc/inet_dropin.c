@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include "mi_cksum.h"
+#include "host_fold.h"
 #include "mi_internal.h"
 
 /* The reference's mbuf prefix (src/sys/sys/mbuf.h:90-98). */
@@ -101,7 +102,7 @@ static void sink_span(struct span_sink *s, const char *p, long n)
 	if (s->dst)
 		memcpy(s->dst + s->total, p, (size_t)n);
 	if (s->fold)
-		s->acc = mi__host_fold_acc(s->acc, mi__host_span_sum(p, (size_t)n), (uint64_t)s->total);
+		s->acc = hf_fold_acc(s->acc, hf_span_sum(p, (size_t)n), (uint64_t)s->total);
 	s->total += n;
 }
 
@@ -182,7 +183,7 @@ static uint16_t host_pseudo(const struct mi_mbuf_view *m, int plen, int off0, ui
 	struct span_sink s = { NULL, 1, 0, 0 };
 
 	walk_pseudo(m, plen, off0, &s);
-	return (uint16_t)~mi__host_fold64(s.acc + pseudo_seed(src, dst, protonum, plen));
+	return (uint16_t)~hf_fold64(s.acc + pseudo_seed(src, dst, protonum, plen));
 }
 
 unsigned short in_cksum_skip(struct mbuf *m0, int len, int skip)
