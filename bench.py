@@ -430,6 +430,7 @@ def main():
 
     if args.config == "tx":  # the TX leg alone (its rocprof / PMC passes)
         row = tx_leg(mi, synth, shard, args, args.steps, dev, dist, backend, rank, world)
+        row.pop("_mm")
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": row["value"], "unit": "GiB/s", "n_gpus": world,
                               "steps": args.steps, "warmup": args.warmup, "ms_per_step": row["ms_per_step"],
@@ -485,7 +486,9 @@ def main():
     # beside the headline with its own roofline.
     for also in args.also:
         if also == "tx":
-            result["config_tx"] = tx_leg(mi, synth, shard, args, K, dev, dist, backend, rank, world)
+            row = tx_leg(mi, synth, shard, args, K, dev, dist, backend, rank, world)
+            per_config_extras(row, "tx", row.pop("_mm"))
+            result["config_tx"] = row
             result["timed_outputs_checked"] = result["timed_outputs_checked"] and result["config_tx"]["timed_outputs_checked"]
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
@@ -605,8 +608,12 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
                                                     device=dev if dist and backend == "nccl" else None)
     alg = float(n) * (2 * frame + 1)  # frame read + frame written + 1 B status
     us = span_us / K
+    import ctypes as C
+    kname = mi.load().mi__tx_kernel_name
+    kname.restype = C.c_char_p
     roof = dict(bound="hbm", achieved=round(alg / us / 1e3, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(alg / us / 1e3 / HBM_PEAK_GBS, 4), traffic=None, kernel="k_tx_copy (mi_cksum_tx_copy)",
+                frac=round(alg / us / 1e3 / HBM_PEAK_GBS, 4), traffic=None,
+                kernel=kname().decode() + " (mi_cksum_tx_copy)",
                 alg_bytes_per_launch=int(alg), avg_launch_us=round(us, 2), streams=len(streams),
                 wall_frac=round(alg * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))
     tf = os.path.join(ROOT, "profiles", "r06", "pmc_traffic_r06.json")
@@ -625,7 +632,8 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
                           "copy + ip_sum + th_sum fused; value = IP datagram bytes checksummed"),
                 rotating_batches=R, footprint_MiB=round(R * per / 2**20, 1), roofline=roof,
                 timed_outputs_checked=checked, frames_checked=covered * n,
-                submit=f"HIP launches over {len(streams)} streams", kernel_env=os.environ.get("MI_CKSUM_TX_KERNEL", "lanes"))
+                submit=f"HIP launches over {len(streams)} streams",
+                _mm=dict(my_bytes=my_bytes, my_elapsed=t1 - t0, job_pkts=job_pkts, elapsed=elapsed))
 
 
 def _oracle_layout(lay: dict) -> dict:

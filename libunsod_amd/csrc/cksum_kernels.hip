@@ -2366,6 +2366,19 @@ int run_dma_code() {
   return c;
 }
 
+// Chunks per lane per pass of the flat run, when forced: MI_CKSUM_PACKED_U
+// (4, 8 or 16) or mi__set_packed_u; 0 = the plan's choice.
+std::atomic<int> g_packed_u{-1};
+int packed_u() {
+  int u = g_packed_u.load(std::memory_order_relaxed);
+  if (u < 0) {
+    const char *e = getenv("MI_CKSUM_PACKED_U");
+    const int v = e ? atoi(e) : 0;
+    u = v == 4 || v == 8 || v == 16 ? v : 0;
+    g_packed_u.store(u, std::memory_order_relaxed);
+  }
+  return u;
+}
 // Pipelined passes of the 2-wave flat run (MI_CKSUM_RUN_PIPE=1; mi__set_run_pipe).
 std::atomic<int> g_run_pipe{-1};
 bool run_pipe() {
@@ -2397,11 +2410,7 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
   // chunks per lane per pass of the flat-run kernel: 8 for packed mixed
   // lengths, 4 for dense minimum-size slots (profiles/packed_u_r01.jsonl);
   // MI_CKSUM_PACKED_U overrides
-  static const int pu_env = [] {
-    const char *e = getenv("MI_CKSUM_PACKED_U");
-    const int u = e ? atoi(e) : 0;
-    return u == 4 || u == 8 || u == 16 ? u : 0;
-  }();
+  const int pu_env = packed_u();
   // the flat-run kernel: hinted packed layouts, and fixed slots that hold
   // little besides the datagram (minimum-size frames: streaming the whole slot
   // costs no more HBM traffic than reading the datagrams' own lines)
@@ -2698,13 +2707,26 @@ Shape pick_tx_shape(uint32_t max_len) {
   return {8, 2};
 }
 
-// Which fused TX kernel: MI_CKSUM_TX_KERNEL = "pair" (k_tx_copy, a lane
-// group per frame, up to two loads per destination chunk) or "wave"
-// (k_tx_wave, a wave per frame, one load per slot).  Read per call so a test
-// can switch.
+// A lane-group TX shape named by MI_CKSUM_TX_SHAPE or mi_cksum_set_shape:
+// k_tx_copy with that shape (the LDS kernel has one shape, 8 x U).
+bool tx_shape_forced() {
+  if (getenv("MI_CKSUM_TX_SHAPE")) return true;
+#define X(G_, U_) if (g_tune.g == G_ && g_tune.u == U_) return true;
+  FOR_TX_GU(X)
+#undef X
+  return false;
+}
+// Which fused TX kernel: MI_CKSUM_TX_KERNEL = "lds" (the default: k_tx_lds,
+// the lane-group gather staged through an LDS ring), "pair" (k_tx_copy, the
+// same gather through VGPRs) or "wave" (k_tx_wave, a wave per frame).  Read
+// per call so a test can switch.  Round 6 A/B, interleaved on one box,
+// 65536 x 1514 B frames (profiles/r06/tx_ab_r06.jsonl): socket chains 47.1 us
+// (lds 2x2) against 49.8 (pair, early loads) and 52.8 (pair); single-segment
+// frames 51.9 against 53.8 and 55.5; deeper rings lose (LDS occupancy).
 int tx_kernel_kind() {
   const char *e = getenv("MI_CKSUM_TX_KERNEL");
-  return e && !strcmp(e, "wave") ? 2 : e && !strcmp(e, "lds") ? 3 : 0;
+  if (!e || !strcmp(e, "lds")) return 3;
+  return !strcmp(e, "wave") ? 2 : 0;
 }
 // The 8x2 lane-group kernel with the next pass's loads issued before this
 // pass's stores (k_tx_copy EL): MI_CKSUM_TX_EARLY=1 / 0, read
@@ -2729,7 +2751,7 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
     hipLaunchKernelGGL((k_tx_wave<2>), dim3(grid_for(t.n, 64)), dim3(kBlock), 0, s, t);
     return launched();
   }
-  if (tx_kernel_kind() == 3) {
+  if (tx_kernel_kind() == 3 && !tx_shape_forced()) {
     // the LDS-staged gather: one wave (8 frames) per workgroup, the same total
     // waves as k_tx_copy's grid
     const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)t.n + 7u) / 8u, 4ull * grid_for(t.n, 8));
@@ -3979,6 +4001,29 @@ int mi__fault_reporter(void) { return g_fault_handler.load(); }
 unsigned long long mi__journal_events(void) { return (unsigned long long)g_jseq.load(); }
 // Diagnostics / tests (not in the public header): waves per workgroup of the
 // flat-run verify kernel (1, 2, 4; speed only, never results).
+// Force the flat run's chunks per lane per pass (4, 8, 16; 0 = automatic);
+// returns the previous setting.
+int mi__set_packed_u(int u) {
+  const int was = packed_u();
+  if (u != 0 && u != 4 && u != 8 && u != 16) return set_err(-EINVAL, "packed U %d", u);
+  g_packed_u.store(u);
+  return was;
+}
+// The fused TX kernel mi_cksum_tx_copy launches now (bench, tools).
+const char *mi__tx_kernel_name(void) {
+  static thread_local char buf[48];
+  const int k = tx_kernel_kind();
+  if (k == 2) return "k_tx_wave<2>";
+  if (k == 3 && !tx_shape_forced()) {
+    int u = 2, r = MI_TX_LDS_R;
+    if (const char *e = getenv("MI_CKSUM_TX_LDS")) (void)sscanf(e, "%dx%d", &u, &r);
+    snprintf(buf, sizeof buf, "k_tx_lds<%d,%d>", u, r);
+    return buf;
+  }
+  const Shape sh = pick_tx_shape(0);
+  snprintf(buf, sizeof buf, "k_tx_copy<%d,%d%s>", sh.g, sh.u, sh.g == 8 && sh.u == 2 && tx_early_loads() ? ",early loads" : "");
+  return buf;
+}
 // Pipelined flat-run passes on (1) / off (0); returns the previous setting.
 int mi__set_run_pipe(int on) {
   const int was = run_pipe() ? 1 : 0;

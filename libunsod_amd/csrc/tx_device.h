@@ -452,8 +452,11 @@ __device__ __forceinline__ void tx_issue(const TxSegs &sg, uint32_t p, int lane,
     cut[u] = c;
   }
 }
+// (on by default since round 6: +6 % on socket chains, +3 % on single
+// segments in the interleaved A/B, profiles/r06/tx_ab_r06.jsonl; round 5 had
+// it off on a misread of the fault record)
 #ifndef MI_TX_EARLY_LOADS
-#define MI_TX_EARLY_LOADS 0
+#define MI_TX_EARLY_LOADS 1
 #endif
 
 // U <= 2 shapes are held to 4 waves per SIMD (128 VGPRs; the descriptor
@@ -1007,7 +1010,7 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
 // would put a vmcnt(0) in front of a plain LDS read while a DMA is pending).
 // One wave per workgroup: the ring is the wave's own.
 #ifndef MI_TX_LDS_R
-#define MI_TX_LDS_R 3
+#define MI_TX_LDS_R 2  // 2 x 2 was the fastest (profiles/r06/tx_ab_r06.jsonl): deeper rings cost waves per CU
 #endif
 template <int U>
 __device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 (&xa)[U], u32x4 (&xb)[U]) {

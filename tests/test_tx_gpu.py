@@ -117,10 +117,11 @@ def test_tx_copy_host_matches_oracle(mode):
         assert np.array_equal(dst[c["dst"].size:], np.zeros(dst.size - c["dst"].size, np.uint8)), name
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lds"])
+@pytest.mark.parametrize("kernel", ["wave", "pair", "lds"])
 def test_tx_kernel_every_case(kernel, monkeypatch):
-    """The wave-per-frame TX kernel (k_tx_wave, MI_CKSUM_TX_KERNEL=wave) and the
-    LDS-staged gather (k_tx_lds, MI_CKSUM_TX_KERNEL=lds) on every
+    """The wave-per-frame TX kernel (k_tx_wave, MI_CKSUM_TX_KERNEL=wave), the
+    lane-group gather through VGPRs (k_tx_copy, =pair) and through an LDS ring
+    (k_tx_lds, =lds, the default) on every
     edge case (socket / single / random / 40-segment chains, padding, far
     headers, short / nobufs / malformed frames, flags and data, UDP 0 ->
     0xffff), byte for byte against the oracle."""
@@ -133,7 +134,7 @@ def test_tx_kernel_every_case(kernel, monkeypatch):
         assert bad.size == 0, (kernel, name, bad.size, bad[:8])
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lds"])
+@pytest.mark.parametrize("kernel", ["wave", "pair", "lds"])
 def test_tx_kernel_full_size(kernel, monkeypatch):
     monkeypatch.setenv("MI_CKSUM_TX_KERNEL", kernel)
     for layout in ("socket", "single"):
@@ -142,3 +143,20 @@ def test_tx_kernel_full_size(kernel, monkeypatch):
         got_dst, got_st = run_gpu(c)
         assert not want_st.any() and np.array_equal(got_st, want_st), layout
         assert np.array_equal(got_dst, want_dst), layout
+
+
+def test_tx_lds_many_frames_per_wave():
+    """The LDS-staged gather (the default TX kernel) with a grid far smaller
+    than the batch: every wave walks many frames through its ring (the
+    grid-stride loop, the ring reused across frames), byte for byte against
+    the oracle on every edge case."""
+    mi.set_shape(0, 0, 3)
+    try:
+        for name, c in CASES:
+            want_dst, want_st = run_oracle(ORC, c)
+            got_dst, got_st = run_gpu(c)
+            assert np.array_equal(got_st, want_st), (name, np.nonzero(got_st != want_st)[0][:8])
+            bad = np.nonzero(got_dst != want_dst)[0]
+            assert bad.size == 0, (name, bad.size, bad[:8])
+    finally:
+        mi.set_shape(0, 0, 0)

@@ -60,7 +60,8 @@ for step in "$@"; do
         python3 bench.py --steps 400 --warmup 5 --config "$cfg" --submit launch --also none --sustain-seconds 0 \
         --cpu-seconds 0 --no-host-path --no-dropin > "$O/prof_$cfg.json" 2> "$O/prof_$cfg.err" || fail "$step" $?
       f=$(ls "$O"/prof_"$cfg"/*/run_kernel_trace.csv "$O"/prof_"$cfg"/run_kernel_trace.csv 2>/dev/null | head -1)
-      python tools/prof_summary.py "$f" > "$O/prof_summary_$cfg.json" || fail "$step" $?
+      kopt=(); [ "$cfg" = tx ] && kopt=(--kernel "${PROF_KERNEL:-k_tx_copy}")
+      python tools/prof_summary.py "$f" "${kopt[@]}" > "$O/prof_summary_$cfg.json" || fail "$step" $?
       cut -c1-400 "$O/prof_summary_$cfg.json" ;;
     pmc)
       cfg=${a:-1500}
