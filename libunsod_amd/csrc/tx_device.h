@@ -1031,8 +1031,11 @@ __device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 
   }
 }
 
+#ifndef MI_TX_LDS_WAVES
+#define MI_TX_LDS_WAVES 4  // waves per SIMD the register budget is held to
+#endif
 template <int U, int R>
-__global__ __launch_bounds__(64) void k_tx_lds(TxDesc t) {
+__global__ __launch_bounds__(64, MI_TX_LDS_WAVES) void k_tx_lds(TxDesc t) {
   constexpr int G = 8;
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");

@@ -25,7 +25,7 @@ CONFIGS = {
     "64": ("64", "k_ipv4_verify_slot64", (1 << 20) * 46 + 5 * (1 << 20)),
     "pareto": ("pareto_u32", "k_ipv4_verify_packed<8, 0, 2>", None),
     # bench.py config_tx: 65536 frames of 1514 B read + written + 1 B status
-    "tx": ("tx", "k_tx_copy<8, 2>", 65536 * (2 * 1514 + 1)),
+    "tx": ("tx", "k_tx_lds<2, 2>", 65536 * (2 * 1514 + 1)),
 }
 
 

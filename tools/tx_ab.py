@@ -29,6 +29,10 @@ VARIANTS = {
     "lds2x3": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x3"),
     "lds2x4": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x4"),
     "lds1x4": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="1x4"),
+    # the 2x2 ring with a smaller grid (mi_cksum_set_shape(0, 0, cap): cap
+    # 4-wave workgroups' worth, i.e. 4 cap one-wave workgroups; 2048 = default)
+    "lds2x2c1024": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2", _cap=1024),
+    "lds2x2c1536": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2", _cap=1536),
 }
 
 
@@ -60,7 +64,9 @@ def main():
         ref = None
         for rnd in range(args.rounds):
             for v in args.variants.split(","):
-                os.environ.update(VARIANTS[v])
+                spec = dict(VARIANTS[v])
+                mi.set_shape(0, 0, spec.pop("_cap", 0))
+                os.environ.update(spec)
 
                 def run(k):
                     for j in range(k):
