@@ -354,7 +354,11 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 // PIPE (round 6, VERDICT r5 "do this" 4): the next pass's loads are issued
 // before this pass is scanned, so a wave streaming a long range keeps a pass
 // in flight while it scans (one more register set).
-template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false, bool PIPE = false>
+// CAP: header windows and last chunks captured from the streamed passes
+// (LDS, 16 B per chunk of a pass) or, false, reloaded through L2 ahead of the
+// stream -- 2 KiB of LDS per wave instead of 10 (round 6: with a tighter
+// register budget, more waves per CU; entry points mi_aql_run<U>w2o).
+template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false, bool PIPE = false, bool CAP = MI_RUN_CAPTURE>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes,
                                             const uint32_t *starts = nullptr, uint32_t nr = 0,
@@ -362,9 +366,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
   constexpr bool TX = MODE == 1, SPAN = MODE == 2;
   constexpr uint32_t W = 64u * U;  // chunks per pass
   __shared__ uint32_t s_q[NW][W];
-#if MI_RUN_CAPTURE
-  __shared__ u32x4 s_c[NW][W];  // the pass's chunks: header windows / last chunks come from here
-#endif
+  __shared__ u32x4 s_c[CAP ? NW : 1][CAP ? W : 1];  // the pass's chunks: header windows / last chunks come from here
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   uint32_t rstride = gridDim.x * NW * 64u;
@@ -458,16 +460,16 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
       const uint32_t cs = st >> 4, ce = en >> 4, h = st & 15u, t = en & 15u;
       // this datagram's header window and last (partial) chunk
       u32x4 hv[3], tv;
-#if MI_RUN_CAPTURE
-      // captured from the run's own passes as they stream by (LDS), not reloaded
+      if constexpr (CAP) {
+        // captured from the run's own passes as they stream by (LDS), not reloaded
 #pragma unroll
-      for (int k = 0; k < 3; ++k) hv[k] = u32x4{0, 0, 0, 0};
-      tv = u32x4{0, 0, 0, 0};
-#else
+        for (int k = 0; k < 3; ++k) hv[k] = u32x4{0, 0, 0, 0};
+        tv = u32x4{0, 0, 0, 0};
+      } else {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) hv[k] = ld16_keep(r, act ? r0 + 16u * (cs + k) : kOOB);
-      tv = ld16_keep(r, act && t ? r0 + 16u * ce : kOOB);
-#endif
+        for (int k = 0; k < 3; ++k) hv[k] = ld16_keep(r, act ? r0 + 16u * (cs + k) : kOOB);
+        tv = ld16_keep(r, act && t ? r0 + 16u * ce : kOOB);
+      }
       uint32_t carry = 0, qs = 0, qe = 0;
       for (uint32_t cb = 0;;) {
         u32x4 vn[PIPE ? U : 1];
@@ -483,9 +485,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
           const uint32_t x = sum4(v[u]);  // chunks past the run load as zeros
           const uint32_t inc = wave_scan(x);
           sq[64u * u + lane] = carry + inc - x;
-#if MI_RUN_CAPTURE
-          s_c[wv][64u * u + lane] = v[u];
-#endif
+          if constexpr (CAP) s_c[wv][64u * u + lane] = v[u];
           carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -493,14 +493,14 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (cs - cb < W) qs = sq[cs - cb];
         if (ce - cb < W) qe = sq[ce - cb];
-#if MI_RUN_CAPTURE
-        if (act) {
+        if constexpr (CAP) {
+          if (act) {
 #pragma unroll
-          for (int k = 0; k < 3; ++k)
-            if (cs + k - cb < W) hv[k] = s_c[wv][cs + k - cb];
-          if (t && ce - cb < W) tv = s_c[wv][ce - cb];
+            for (int k = 0; k < 3; ++k)
+              if (cs + k - cb < W) hv[k] = s_c[wv][cs + k - cb];
+            if (t && ce - cb < W) tv = s_c[wv][ce - cb];
+          }
         }
-#endif
         cb += W;
         if (cb >= nch) break;
 #pragma unroll
@@ -584,6 +584,15 @@ __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Des
                                                                 uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
                                                                 uint32_t abs_lanes) {
   packed_body<U, MODE, NW, false, PIPE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+}
+#ifndef MI_RUN_OCC_WAVES
+#define MI_RUN_OCC_WAVES 5
+#endif
+template <int U, int WV = (U == 4 ? MI_RUN_OCC_WAVES : 4)>
+__global__ __launch_bounds__(128, WV) void k_ipv4_verify_packed_occ(Desc d, uint16_t *ip_out, uint16_t *l4_out,
+                                                                uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
+                                                                uint32_t abs_lanes) {
+  packed_body<U, 0, 2, false, false, false>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
 template <int U, int NW>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_ranges(Desc d, uint16_t *ip_out, uint16_t *l4_out,
@@ -1458,6 +1467,15 @@ MI_AQL_RUN_W(8, 2)
   }
 MI_AQL_RUN_WP(4)
 MI_AQL_RUN_WP(8)
+// (the same, header windows reloaded instead of captured, held to
+// MI_RUN_OCC_WAVES waves per SIMD: mi_aql_run<U>w2o)
+#define MI_AQL_RUN_WO(U_, WV_)                                                                          \
+  extern "C" __global__ __launch_bounds__(128, WV_) void mi_aql_run##U_##w2o(                            \
+      Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, uint32_t *bad) {                                 \
+    packed_body<U_, 0, 2, false, false, false>(d, ip, l4, st, bad, SpanSeeds{}, 0u);                     \
+  }
+MI_AQL_RUN_WO(4, MI_RUN_OCC_WAVES)
+MI_AQL_RUN_WO(8, 4)  // (U = 8 at 5 waves per SIMD spills)
 #define MI_AQL_RUN(U_)                                                                                  \
   extern "C" __global__ PACKED_BOUNDS void mi_aql_run##U_(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st, \
                                                            uint32_t *bad) {                             \
@@ -2339,6 +2357,7 @@ struct Plan {
   int run_nw = 4;  // kPlanRun: waves per workgroup (k_ipv4_verify_packed<U, 0, NW>)
   int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
   bool pipe = false;  // kPlanRun, 2 waves: the pipelined passes (packed_body PIPE)
+  bool occ = false;   // kPlanRun, 2 waves: header windows reloaded, 5 waves per SIMD (mi_aql_run<U>w2o)
 };
 
 // The LDS-DMA flat run (k_ipv4_verify_run_dma) for packed batches with offset
@@ -2378,6 +2397,17 @@ int packed_u() {
     g_packed_u.store(u, std::memory_order_relaxed);
   }
   return u;
+}
+// The occupancy variant of the 2-wave flat run (MI_CKSUM_RUN_OCC=1; mi__set_run_occ).
+std::atomic<int> g_run_occ{-1};
+bool run_occ() {
+  int v = g_run_occ.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char *e = getenv("MI_CKSUM_RUN_OCC");
+    v = e && e[0] == '1' ? 1 : 0;
+    g_run_occ.store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
 }
 // Pipelined passes of the 2-wave flat run (MI_CKSUM_RUN_PIPE=1; mi__set_run_pipe).
 std::atomic<int> g_run_pipe{-1};
@@ -2424,6 +2454,7 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
     Plan pl{kPlanRun, {0, 0}, pu_env ? pu_env : dense_slots ? 4 : 8};
     pl.run_nw = pl.run_u == 16 ? 4 : run_waves();
     pl.pipe = pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_pipe();
+    pl.occ = !pl.pipe && pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_occ();
     // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
     // offset / length arrays: batches whose arrays reach kOOB take the register
     // kernel, whose descriptor reads are 64-bit)
@@ -2568,6 +2599,14 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
     VLAUNCH((k_ipv4_verify_packed<U_, 0, NW_>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);         \
     return launched();                                                                                       \
   }
+    if (pl.occ && pl.run_nw == 2 && pl.run_u == 4) {
+      VLAUNCH((k_ipv4_verify_packed_occ<4>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      return launched();
+    }
+    if (pl.occ && pl.run_nw == 2 && pl.run_u == 8) {
+      VLAUNCH((k_ipv4_verify_packed_occ<8>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
+      return launched();
+    }
     if (pl.pipe && pl.run_nw == 2 && pl.run_u == 4) {
       VLAUNCH((k_ipv4_verify_packed<4, 0, 2, true>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
       return launched();
@@ -2806,6 +2845,7 @@ enum AqlKernelId {
   MI_DEAL_SHAPES(X)
 #undef X
   kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2, kAqlRun4w2p, kAqlRun8w2p,
+  kAqlRun4w2o, kAqlRun8w2o,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2819,7 +2859,7 @@ const char *const kAqlNames[kAqlKernels] = {
     MI_DEAL_SHAPES(X)
 #undef X
     "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
-    "mi_aql_run4w2p", "mi_aql_run8w2p",
+    "mi_aql_run4w2p", "mi_aql_run8w2p", "mi_aql_run4w2o", "mi_aql_run8w2o",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2833,7 +2873,8 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #undef X
     (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
     (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
-    (const void *)mi_aql_run4w2p, (const void *)mi_aql_run8w2p,
+    (const void *)mi_aql_run4w2p, (const void *)mi_aql_run8w2p, (const void *)mi_aql_run4w2o,
+    (const void *)mi_aql_run8w2o,
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3160,6 +3201,7 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks, b
   }
   if (pl.kind == kPlanRun) {
     if (pl.run_nw == 1) *id = pl.run_u == 4 ? kAqlRun4w1 : kAqlRun8w1;
+    else if (pl.run_nw == 2 && pl.occ) *id = pl.run_u == 4 ? kAqlRun4w2o : kAqlRun8w2o;
     else if (pl.run_nw == 2 && pl.pipe) *id = pl.run_u == 4 ? kAqlRun4w2p : kAqlRun8w2p;
     else if (pl.run_nw == 2) *id = pl.run_u == 4 ? kAqlRun4w2 : kAqlRun8w2;
     else *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
@@ -3276,7 +3318,8 @@ void aql_fill_raw(uint8_t *ka, const void *args, uint32_t nargs, unsigned blocks
 unsigned aql_wg(int id) {
   switch (id) {
     case kAqlRun4w1: case kAqlRun8w1: return 64;
-    case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: return 128;
+    case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: case kAqlRun4w2o: case kAqlRun8w2o:
+      return 128;
     case kAqlScalar: return kScalarThreads;
     default: return kBlock;
   }
@@ -4024,6 +4067,12 @@ const char *mi__tx_kernel_name(void) {
   snprintf(buf, sizeof buf, "k_tx_copy<%d,%d%s>", sh.g, sh.u, sh.g == 8 && sh.u == 2 && tx_early_loads() ? ",early loads" : "");
   return buf;
 }
+// The flat run's occupancy variant on (1) / off (0); returns the previous setting.
+int mi__set_run_occ(int on) {
+  const int was = run_occ() ? 1 : 0;
+  g_run_occ.store(on ? 1 : 0);
+  return was;
+}
 // Pipelined flat-run passes on (1) / off (0); returns the previous setting.
 int mi__set_run_pipe(int on) {
   const int was = run_pipe() ? 1 : 0;
@@ -4261,6 +4310,7 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
     snprintf(buf, sizeof buf,
              pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>"
              : pl.pipe      ? "k_ipv4_verify_packed<%d,%d waves,pipelined>"
+             : pl.occ       ? "k_ipv4_verify_packed_occ<%d,%d waves>"
                             : "k_ipv4_verify_packed<%d,%d waves>",
              pl.run_u, pl.run_nw);
   else if (pl.kind == kPlanShape)

@@ -1034,8 +1034,13 @@ __device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 
 #ifndef MI_TX_LDS_WAVES
 #define MI_TX_LDS_WAVES 4  // waves per SIMD the register budget is held to
 #endif
+// (a deeper ring's LDS holds a CU below MI_TX_LDS_WAVES per SIMD anyway:
+// 160 KiB / (2 U R KiB per wave) / 4 SIMDs)
+constexpr int tx_lds_waves(int u, int r) {
+  return 160 / (2 * u * r) / 4 < MI_TX_LDS_WAVES ? 160 / (2 * u * r) / 4 : MI_TX_LDS_WAVES;
+}
 template <int U, int R>
-__global__ __launch_bounds__(64, MI_TX_LDS_WAVES) void k_tx_lds(TxDesc t) {
+__global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
   constexpr int G = 8;
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");

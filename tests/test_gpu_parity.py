@@ -351,6 +351,44 @@ def test_packed_layout_golden(golden):
     assert int(r["bad"].item()) == int((g["ver_st"] != 0).sum())
 
 
+@pytest.mark.parametrize("variant", [(4, 0, 0), (8, 1, 0), (4, 1, 0), (8, 0, 1), (4, 0, 1)])
+def test_packed_variants_golden(golden, variant):
+    """The flat-run kernel's round-6 variants -- chunks per pass U, pipelined
+    passes (mi__set_run_pipe), header windows reloaded at a tighter register
+    budget (mi__set_run_occ) -- on the golden RX batch (HIP launches) and on a
+    Pareto batch through the AQL engine, bit-exact."""
+    import ctypes as C
+    lib = mi.load()
+    for f in ("mi__set_packed_u", "mi__set_run_pipe", "mi__set_run_occ"):
+        getattr(lib, f).restype = C.c_int
+        getattr(lib, f).argtypes = [C.c_int]
+    u, pipe, occ = variant
+    was = (lib.mi__set_packed_u(u), lib.mi__set_run_pipe(pipe), lib.mi__set_run_occ(occ))
+    try:
+        test_packed_layout_golden(golden)
+        n = 20000
+        lens = synth.pareto_lengths(n, seed=23)
+        offs = synth.packed_offsets(lens, first_off=2)
+        b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=24)
+        _, ref = aligned(b0["buf"])
+        ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32), nthreads=8)
+        ref[offs[::97].astype(np.int64) + 33] ^= 0x21
+        ip_o, l4_o, st_o = ORC.ipv4_verify_batch(ref, n, offs=offs, flen=lens.astype(np.uint32), nthreads=8)
+        b = mi.PktBatch(dev_tensor(ref), n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(lens.astype(np.int32)),
+                        packed=True, offs32=True)
+        outs = [dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"), l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                     status=torch.zeros(n, dtype=torch.uint8, device="cuda"))]
+        rep = mi.VerifyRepeat([b], outs, nstreams=2, engine="aql")
+        rep.run(3)
+        rep.close()
+        assert np.array_equal(cpu(outs[0]["ip"]), ip_o) and np.array_equal(cpu(outs[0]["l4"]), l4_o)
+        assert np.array_equal(cpu(outs[0]["status"]), st_o)
+    finally:
+        lib.mi__set_packed_u(was[0])
+        lib.mi__set_run_pipe(was[1])
+        lib.mi__set_run_occ(was[2])
+
+
 @pytest.mark.parametrize("layout", ["packed", "shuffled", "gappy"])
 def test_packed_hint_any_layout(layout):
     """The packed kernel is exact on real packed batches and falls back (still
