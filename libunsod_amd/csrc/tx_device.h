@@ -1004,9 +1004,11 @@ __global__ __launch_bounds__(kBlock, MI_TX_WAVE_WAVES) void k_tx_wave(TxDesc t) 
 //
 // Ordering (MI355X_MICROARCH.md, LDS-DMA): only the issuing wave's vmcnt
 // orders a ds_read behind a DMA.  Pass p's 2U DMAs are followed by the 2U of
-// each of the R-1 passes issued after them, so vmcnt <= 2U(R-1) retires them
-// (stores and descriptor loads in between only add to the count: waiting for
-// 2U(R-1) is conservative).  The ring's reads are inline asm (the compiler
+// each pass issued after them (gi - p - 1 of them, at most R - 1; a pass no
+// lane of the wave has is not issued), so vmcnt <= 2U(gi - p - 1) retires
+// them (stores and descriptor loads in between only add to the count, so the
+// wait is conservative; wait_vm_ladder turns the uniform count into an
+// s_waitcnt immediate).  The ring's reads are inline asm (the compiler
 // would put a vmcnt(0) in front of a plain LDS read while a DMA is pending).
 // One wave per workgroup: the ring is the wave's own.
 #ifndef MI_TX_LDS_R
@@ -1146,9 +1148,15 @@ __global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
       const uint32_t D0 = seg_delta(0), D1 = seg_delta(1), D2 = seg_delta(2), D3 = seg_delta(3);
       const uint32_t lim = t.src_bytes - 16u;
       const TxSegs sg{S1, S2, S3, (int)len, D0, D1, D2, D3, lim};
-      // pass q's 2U DMAs into ring slot q % R (lanes past their frame's last
-      // pass, and loads a chunk does not need, read nothing: offset kOOB)
+      // pass q's 2U DMAs into ring slot q % R, if any lane of the wave has a
+      // pass q (lanes past their frame's last pass, and loads a chunk does not
+      // need, read nothing: offset kOOB).  gi counts the passes issued, pc
+      // the passes consumed (both wave-uniform).
+      uint32_t gi = 0, pc = 0;
+      bool brk = false;
       auto issue = [&](uint32_t q) {
+        if (!__any(q < npass)) return;
+        ++gi;
         const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(q % (uint32_t)R));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1164,7 +1172,10 @@ __global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
 #pragma unroll
       for (int q = 0; q < R; ++q) issue((uint32_t)q);
       for (uint32_t p = 0; p < npass; ++p) {
-        __builtin_amdgcn_s_waitcnt(waitcnt_vm(2 * U * (R - 1)));  // pass p has landed
+        // pass p has landed: the DMAs of the gi - p - 1 passes issued after it
+        // may still be in flight
+        wait_vm_ladder<2 * U, R - 1>((uint32_t)__builtin_amdgcn_readfirstlane((int)(gi - pc - 1u)));
+        ++pc;
         const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(p % (uint32_t)R));
         u32x4 xa[U], xb[U], v[U];
         tx_ring_read<U>(&s_ring[sl][0][0], (int)threadIdx.x & 63, xa, xb);
@@ -1186,7 +1197,10 @@ __global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
           const uint32_t pip = l3 + 10u, pl4 = l3 + at;
           const bool l4s = do_l4 && (uint64_t)at + 2u <= ip_mlen;
           const uint32_t need = max(do_ip ? pip + 2u : 0u, l4s ? pl4 + 2u : 0u);
-          if ((uint64_t)need + h > 16ull * G) break;  // a sum field beyond the held chunks: generic path
+          if ((uint64_t)need + h > 16ull * G) {  // a sum field beyond the held chunks: generic path
+            brk = true;
+            break;
+          }
           done = true;
           held = v[0];
         }
@@ -1222,9 +1236,13 @@ __global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
         if (ci < nch) store_chunk(rd, c0 + 16u * ci, held, -cs, (int)len - cs);
         if (lane == 0) st_u8(ta.status, i, (ok ? 0u : MI_TX_NOSUM) | (do_l4 && !l4_store ? MI_TX_L4_SKIPPED : 0u));
       }
-      // the ring's over-issued passes (offset kOOB: zeros) land before the
-      // next frame writes the ring or s_seg
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+      // Every pass the wave issued was below the longest frame's pass count,
+      // so the groups with that frame have read them all -- unless a group
+      // left for the generic path at p == 0: then passes issued for it may
+      // still be in flight, and they land before the ring is written again or
+      // the wave ends.  (gi / pc are equal in all lanes still in the loop,
+      // stale in lanes that left it: they are not tested here.)
+      if (__any(brk)) __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
       __builtin_amdgcn_wave_barrier();
     }
     prefetch2();
