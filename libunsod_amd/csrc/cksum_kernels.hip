@@ -2805,6 +2805,11 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
   }
     X(2, 2) X(2, 3) X(2, 4) X(1, 4)
 #undef X
+    // U = 1, R = 3 at 5 waves per SIMD (96 VGPRs, no scratch; 6 KiB of ring)
+    if (u == 1 && r == 3) {
+      hipLaunchKernelGGL((k_tx_lds<1, 3, 5>), dim3(grid ? grid : 1u), dim3(64), 0, s, t);
+      return launched();
+    }
     return set_err(-EINVAL, "no LDS TX kernel %dx%d", u, r);
   }
   const int grid = grid_for(t.n, sh.g);

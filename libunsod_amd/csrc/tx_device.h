@@ -1041,8 +1041,8 @@ __device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 
 constexpr int tx_lds_waves(int u, int r) {
   return 160 / (2 * u * r) / 4 < MI_TX_LDS_WAVES ? 160 / (2 * u * r) / 4 : MI_TX_LDS_WAVES;
 }
-template <int U, int R>
-__global__ __launch_bounds__(64, tx_lds_waves(U, R)) void k_tx_lds(TxDesc t) {
+template <int U, int R, int WV = tx_lds_waves(U, R)>
+__global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
   constexpr int G = 8;
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
