@@ -108,6 +108,26 @@ def test_segment_table_extent_bounds_the_walk():
     assert not np.array_equal(got, full)
 
 
+def test_huge_segment_index_reads_nothing():
+    """a segment index of 2^30 used to wrap the 32-bit byte offsets
+    of both tables (4 * i, 8 * i) to 0 and read segment 0's m_len / m_data --
+    a plausible wrong checksum.  Offsets now clamp to the out-of-range value
+    and read (m_data 0, m_len 0): the last chain, pointed at segments 2^30 and
+    2^30 + 1, is an empty chain (in_cksum_skip of nothing: 0xffff) and every
+    other chain is unchanged."""
+    chains = _chains(seed=9, n=64)
+    cb = mi.ChainBatch(chains)
+    length = [sum(len(s) for s, _ in ch) for ch in chains]
+    skip = [0] * len(chains)
+    want = np.array([ORC.chain_skip(ch, ln, 0) for ch, ln in zip(chains, length)], np.int64)
+    n = cb.n
+    cb.pkt_seg[n - 1] = 1 << 30
+    cb.pkt_seg[n] = (1 << 30) + 2
+    got = _chain_call(cb, length, skip, 1 << 30)
+    assert np.array_equal(got[:n - 1], want[:n - 1])
+    assert got[n - 1] == 0xFFFF
+
+
 @pytest.mark.parametrize("kind", ["1500", "64", "pareto", "pareto-dma"])
 def test_outputs_never_written_past_n(kind):
     """Outputs sit at the front of larger poisoned tensors: nothing past n
