@@ -181,3 +181,35 @@ def test_page_buffer_is_page_granular():
     a[:] = 1
     pa, pb = a.ctypes.data, b.ctypes.data
     assert pa + 8192 <= pb or pb + 4096 <= pa  # no page shared
+
+
+from oracle.pyoracle import Oracle, available  # noqa: E402  (the checker)
+
+
+@pytest.mark.skipif(not available("reference"), reason="oracle/_ref not built")
+def test_random_chains_match_the_reference():
+    """Property test beyond the golden vectors: 3000 random chains (1-6 mbufs,
+    0-4100 bytes each, every address parity, zero-length mbufs, skips and
+    lengths past the chain's end) through in_cksum_skip and
+    in_cksum_pseudo_header, against the reference's own in_cksum.c
+    (oracle/_ref) on the same mbuf layouts.  Long spans take the vector body,
+    short ones the word loop; both stream-parity branches are hit."""
+    ref = Oracle("reference")
+    rng = np.random.default_rng(20260)
+    for _ in range(3000):
+        k = int(rng.integers(1, 7))
+        segs = []
+        for _ in range(k):
+            ln = int(rng.choice([0, int(rng.integers(1, 64)), int(rng.integers(64, 4100))]))
+            segs.append((rng.integers(0, 256, ln, dtype=np.uint8).tobytes(), int(rng.integers(0, 8))))
+        total = sum(len(s) for s, _ in segs)
+        skip = int(rng.integers(0, min(total, 60) + 1))
+        length = int(rng.integers(skip, total + 40 + 1))
+        m = mi.MbufChain(segs)
+        assert mi.in_cksum_skip(m, length, skip) == ref.chain_skip(segs, length, skip), (segs, length, skip)
+        if len(segs[0][0]) >= 20:
+            plen = int(rng.integers(0, total + 1))
+            src, dst = (int(x) for x in rng.integers(0, 1 << 32, 2, dtype=np.uint64))
+            proto = int(rng.choice([6, 17]))
+            assert (mi.in_cksum_pseudo_header(m, plen, 20, src, dst, proto)
+                    == ref.chain_pseudo(segs, plen, 20, src, dst, proto))
