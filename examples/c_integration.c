@@ -6,7 +6,8 @@
  *      layout of src/sys/sys/mbuf.h:90-98: m_next@0, m_data@16, m_len@24),
  *      checked against the SURVEY.md 8(a) known answers, called from several
  *      threads at once (the reference calls them from the dpdk_rx kthread, the
- *      application threads and the callout thread concurrently).
+ *      application threads and the callout thread concurrently), folded on
+ *      the CPU (the default) and through the GPU drop-in service.
  *   2. (b2) a host-memory RX burst as the DPDK driver holds it (rte_mbuf slots
  *      of 2176 B, IP header at +142): TX-finalized, registered, verified in
  *      place over PCIe, then one corrupted datagram detected.
@@ -112,12 +113,21 @@ int main(void)
 	CHECK(in_cksum_hdr((const struct ip *)(hb + 33)) == 0xb861, "KAT4 (odd address)");
 	CHECK(in_pseudo(0x0101a8c0u, 0x0201a8c0u, 0xce050000u) == 0x2289, "KAT10");
 
-	/* the drop-ins from 8 threads at once */
-	pthread_t th[8];
-	for (int t = 0; t < 8; t++)
-		pthread_create(&th[t], NULL, dropin_thread, (void *)(intptr_t)t);
-	for (int t = 0; t < 8; t++)
-		pthread_join(th[t], NULL);
+	/* the drop-ins from 8 threads at once: folded on the calling cores (the
+	 * default, MI_DROPIN_HOST), then through the GPU's drop-in service
+	 * (MI_DROPIN_GPU) -- with no call answered by the host fold after a GPU
+	 * error */
+	const uint64_t degraded = mi_cksum_dropin_degraded();
+	for (int mode = MI_DROPIN_HOST; mode <= MI_DROPIN_GPU; mode++) {
+		const int was = mi_cksum_set_dropin_mode(mode);
+		pthread_t th[8];
+		for (int t = 0; t < 8; t++)
+			pthread_create(&th[t], NULL, dropin_thread, (void *)(intptr_t)t);
+		for (int t = 0; t < 8; t++)
+			pthread_join(th[t], NULL);
+		mi_cksum_set_dropin_mode(was);
+	}
+	CHECK(mi_cksum_dropin_degraded() == degraded, "GPU-mode drop-ins degraded to the host fold");
 
 	/* a host-memory RX burst: 1024 x 1500 B datagrams in rte_mbuf slots,
 	 * checksummed on the way out by the software TX path through the drop-ins

@@ -2798,6 +2798,11 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
     // call: A/B in one process); default 2 x MI_TX_LDS_R
     int u = 2, r = MI_TX_LDS_R;
     if (const char *e = getenv("MI_CKSUM_TX_LDS")) (void)sscanf(e, "%dx%d", &u, &r);
+    // the cut cache (k_tx_lds CC): MI_CKSUM_TX_LDS = "2x2c"
+    if (const char *e = getenv("MI_CKSUM_TX_LDS"); e && u == 2 && r == 2 && strchr(e, 'c')) {
+      hipLaunchKernelGGL((k_tx_lds<2, 2, tx_lds_waves(2, 2), true>), dim3(grid ? grid : 1u), dim3(64), 0, s, t);
+      return launched();
+    }
 #define X(U_, R_)                                                                         \
   if (u == U_ && r == R_) {                                                               \
     hipLaunchKernelGGL((k_tx_lds<U_, R_>), dim3(grid ? grid : 1u), dim3(64), 0, s, t);    \

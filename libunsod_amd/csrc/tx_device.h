@@ -1041,13 +1041,48 @@ __device__ __forceinline__ void tx_ring_read(const u32x4 *slot, int lane, u32x4 
 constexpr int tx_lds_waves(int u, int r) {
   return 160 / (2 * u * r) / 4 < MI_TX_LDS_WAVES ? 160 / (2 * u * r) / 4 : MI_TX_LDS_WAVES;
 }
-template <int U, int R, int WV = tx_lds_waves(U, R)>
+// CC (cut cache): each chunk's cut (tx_cut: where its segments meet, the
+// frame's ends, the slow case) is worked out once, when its pass is issued,
+// and kept packed in LDS beside the ring for the build, instead of being
+// computed again then (the SQ counters put the kernel's VALU ~60 % busy,
+// profiles/r06/sq_counters_tx_r06.jsonl).
+__device__ __forceinline__ void lds_wr32(const void *p, uint32_t x) {
+  asm volatile("ds_write_b32 %0, %1" : : "v"(lds_addr(p)), "v"(x) : "memory");
+}
+template <int U>
+__device__ __forceinline__ void lds_rd32_u(const uint32_t *row, int lane, uint32_t (&x)[U]) {
+  static_assert(U == 1 || U == 2, "cut reads for U = 1, 2");
+  if constexpr (U == 1) {
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(x[0]) : "v"(lds_addr(row + lane)) : "memory");
+  } else {
+    asm volatile("ds_read_b32 %0, %2\n\tds_read_b32 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(x[0]), "=&v"(x[1])
+                 : "v"(lds_addr(row + lane)), "v"(lds_addr(row + 64 + lane))
+                 : "memory");
+  }
+}
+__device__ __forceinline__ uint32_t cut_pack(const TxCut &c) {
+  return (uint32_t)(min(max(c.B, -1), 17) + 1) | (c.two ? 32u : 0u) | (c.clip ? 64u : 0u) | (c.slow ? 128u : 0u);
+}
+// (only what tx_build reads: q0, B and the three cases)
+__device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
+  TxCut c;
+  c.q0 = q0;
+  c.B = (int)(k & 31u) - 1;
+  c.A1 = c.A2 = 0;
+  c.two = k & 32u;
+  c.clip = k & 64u;
+  c.slow = k & 128u;
+  return c;
+}
+template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false>
 __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
   constexpr int G = 8;
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
   __shared__ uint32_t s_seg[NG][kTxSeg][2];
   __shared__ u32x4 s_ring[R][2 * U][64];  // pass slot q % R: chunk u's A1 loads, then its A2 loads
+  __shared__ uint32_t s_cut[CC ? R : 1][CC ? U : 1][64];  // CC: pass slot q % R's packed cuts
   typedef __attribute__((address_space(3))) void *lds_ptr;
   Desc ds{}, dd{};
   ds.base = t.src;
@@ -1166,6 +1201,7 @@ __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
                                                   live && c.q0 < sg.L ? c.A1 : kOOB, 0, 0, MI_TX_LOAD_AUX);
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr)&s_ring[sl][2 * u + 1][0], 16,
                                                   live && c.two ? c.A2 : kOOB, 0, 0, MI_TX_LOAD_AUX);
+          if constexpr (CC) lds_wr32(&s_cut[sl][u][threadIdx.x & 63u], cut_pack(c));
         }
       };
       u32x4 held{0, 0, 0, 0};
@@ -1179,8 +1215,17 @@ __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
         const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(p % (uint32_t)R));
         u32x4 xa[U], xb[U], v[U];
         tx_ring_read<U>(&s_ring[sl][0][0], (int)threadIdx.x & 63, xa, xb);
+        if constexpr (CC) {
+          uint32_t pk[U];
+          lds_rd32_u<U>(&s_cut[sl][0][0], (int)threadIdx.x & 63, pk);
 #pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
+          for (int u = 0; u < U; ++u)
+            v[u] = tx_build(sg, cut_unpack(pk[u], (int)(16u * (p * (G * U) + u * G + lane)) - (int)h), xa[u], xb[u], rs);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            v[u] = tx_build(sg, tx_cut(sg, p * (G * U) + u * G + lane, h), xa[u], xb[u], rs);
+        }
         issue(p + R);  // the slot's reads have returned (lgkmcnt(0) in tx_ring_read)
         if (p == 0) {
           prefetch2();
