@@ -528,9 +528,9 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
     649-672 / in_delayed_cksum :958-983) over 65536 x 1500 B IPv4/TCP frames whose
     chains have the socket layout tcp_output builds (a header mbuf + payload
     pieces in 2 KiB socket-buffer clusters, synth.build_tx_chains), copied into
-    2176 B rte_mbuf slots (data at +128).  A step = one launch over one batch
-    (HIP launches alternating over two streams; the engine of the RX legs has
-    no TX entry point).  Same bracket as the RX legs: barrier + synchronize,
+    2176 B rte_mbuf slots (data at +128).  A step = one launch over one batch,
+    submitted like the RX legs' (a prepared handle, mi_cksum_tx_repeat_create;
+    AQL packets over two queues by default).  Same bracket as the RX legs: barrier + synchronize,
     K launches, synchronize, max over ranks; outputs poisoned before and checked
     after (every covered batch's status 0 and its slots verifying clean under the
     RX kernel).  Weak-scaled: every rank copies its own batch."""
@@ -548,12 +548,22 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
         tb = mi.TxBatch(src, d["seg_off"], d["seg_len"], d["pkt_seg"], d["pkt_len"], dst, dst_stride=stride,
                         dst_first=dst_first, room=stride - dst_first, l3_off=l3, max_len=frame)
         batches.append((tb, torch.empty(n, dtype=torch.uint8, device=dev)))
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
+    torch.cuda.synchronize()  # (the AQL engine does not order itself after torch's streams)
+    nst = max(1, args.streams)
+    # The K launches go out through a prepared TX handle (mi_cksum_tx_repeat_*),
+    # by default as prebuilt AQL packets of the default TX kernel in the
+    # handle's own HSA queues -- the RX legs' submission; --submit launch: HIP
+    # launches alternating over the handle's streams.
+    engine_note = None
+    try:
+        rep = mi.TxRepeat([b for b, _ in batches], [st for _, st in batches], nstreams=nst,
+                          engine="aql" if args.submit == "aql" else "hip")
+    except mi.MiCksumError as e:
+        engine_note = f"AQL engine unavailable ({e}); HIP launches"
+        rep = mi.TxRepeat([b for b, _ in batches], [st for _, st in batches], nstreams=nst)
 
-    def run(k: int):
-        for j in range(k):
-            tb, st = batches[j % R]
-            mi.tx_copy(tb, status=st, stream=streams[j % len(streams)])
+    def run(k: int, timed: bool = False):
+        rep.run(k, timed=timed)
 
     def verify_slots(tb) -> int:
         """Frames of tb's slots that do NOT verify under the RX kernel."""
@@ -567,35 +577,29 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
     if verify_slots(batches[0][0]) or bool((batches[0][1] != 0).any()):
         raise SystemExit(f"rank {rank}: TX copy output does not verify")
     tw = time.perf_counter()
-    run(max(args.warmup, 1))
+    run(max(args.warmup, 1), timed=True)
     while time.perf_counter() - tw < args.settle:
-        run(50)
+        run(50, timed=True)
+    for _ in range(args.warm_regions):  # bracketed like the timed region
+        torch.cuda.synchronize()
+        run(K, timed=True)
         torch.cuda.synchronize()
     torch.cuda.synchronize()
     for tb, st in batches:  # poison: covered batches must come back copied + summed
         tb.dst.zero_()
         st.fill_(0xFF)
     torch.cuda.synchronize()
-    ev0 = [torch.cuda.Event(enable_timing=True) for _ in streams]
-    ev1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    gate = torch.cuda.Event()
-    gate.record(streams[0])
-    for s_ in streams[1:]:
-        s_.wait_event(gate)
-    for e, s_ in zip(ev0, streams):
-        e.record(s_)
-    run(K)
-    for e, s_ in zip(ev1, streams):
-        e.record(s_)
+    run(K, timed=True)  # submission + completion + wait
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    span_us = max(ev0[0].elapsed_time(e) for e in ev1) * 1e3  # events on the launch streams
+    span_us = rep.span()  # GPU span of the K passes (dispatch timestamps / events), read after the region
+    rep.close()
     covered = min(K, R)
     bad_frames = sum(verify_slots(batches[j][0]) for j in range(covered))
     st_ok = all(bool((batches[j][1] == 0).all()) for j in range(covered))
@@ -614,8 +618,10 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
     roof = dict(bound="hbm", achieved=round(alg / us / 1e3, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(alg / us / 1e3 / HBM_PEAK_GBS, 4), traffic=None,
                 kernel=kname().decode() + " (mi_cksum_tx_copy)",
-                alg_bytes_per_launch=int(alg), avg_launch_us=round(us, 2), streams=len(streams),
+                alg_bytes_per_launch=int(alg), avg_launch_us=round(us, 2), streams=nst,
                 wall_frac=round(alg * K / (t1 - t0) / 1e9 / HBM_PEAK_GBS, 4))
+    if rep.engine == "aql" and engine_note is None:
+        roof["kernel"] = kname().decode() + " (its AQL entry point mi_aql_tx_lds)"
     tf = os.path.join(ROOT, "profiles", "r06", "pmc_traffic_r06.json")
     try:
         ent = json.load(open(tf)).get("tx") if os.path.exists(tf) else None
@@ -632,7 +638,8 @@ def tx_leg(mi, synth, shard, args, K: int, dev, dist, backend: str, rank: int, w
                           "copy + ip_sum + th_sum fused; value = IP datagram bytes checksummed"),
                 rotating_batches=R, footprint_MiB=round(R * per / 2**20, 1), roofline=roof,
                 timed_outputs_checked=checked, frames_checked=covered * n,
-                submit=f"HIP launches over {len(streams)} streams",
+                submit=engine_note or (f"prepared TX handle, AQL packets ({nst} own HSA queues)" if rep.engine == "aql"
+                                       else f"prepared TX handle, HIP launches over {nst} streams"),
                 _mm=dict(my_bytes=my_bytes, my_elapsed=t1 - t0, job_pkts=job_pkts, elapsed=elapsed))
 
 

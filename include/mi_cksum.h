@@ -377,6 +377,7 @@ void mi_cksum_repeat_destroy(mi_repeat *r);
  * (mi_cksum_ipv4_finalize in place; outputs unused). */
 #define MI_REPEAT_OP_VERIFY   0u
 #define MI_REPEAT_OP_FINALIZE 1u
+#define MI_REPEAT_OP_TX_COPY  2u  /* set by mi_cksum_tx_repeat_create only */
 int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op);
 /* How a run submits its passes.
  * MI_REPEAT_ENGINE_HIP (default): HIP launches alternating over the handle's
@@ -493,6 +494,19 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream);
  */
 #define MI_TX_HOST_STAGED 1u
 int mi_cksum_tx_copy_host(const mi_tx_batch *b, uint8_t *status, uint32_t flags);
+
+/*
+ * mi_cksum_tx_copy prepared once for a transmit loop that re-submits the same
+ * rings (the mi_cksum_repeat_* handle, op MI_REPEAT_OP_TX_COPY): pass k copies
+ * batch b[k % nb] with its sums into its slots, status into status[k % nb]
+ * (device arrays), over the handle's nstreams streams; run / span / destroy
+ * as for a verify handle.  mi_cksum_repeat_set_engine(r, MI_REPEAT_ENGINE_AQL)
+ * sends the passes as prebuilt AQL packets of the default TX kernel
+ * (-ENOTSUP while MI_CKSUM_TX_KERNEL / _TX_LDS / _TX_SHAPE select another).
+ * Same bytes and status as mi_cksum_tx_copy.  nb <= 1024, every batch n > 0.
+ */
+int mi_cksum_tx_repeat_create(const mi_tx_batch *b, uint32_t nb, uint8_t *const *status,
+                              uint32_t nstreams, mi_repeat **out);
 
 /*
  * Host-resident batch (the path's real start and end: DPDK mbufs in host

@@ -10,7 +10,7 @@ from ._lib import (LIB_PATH, MI_SPAN_ABS, MI_SPAN_STREAM, MI_ST_IP_BAD, MI_ST_L4
 from .api import (ChainBatch, MbufChain, chain_batch, PktBatch, device_count, host_register, host_unregister, in_addword, in_cksum,
                   in_cksum_hdr, in_cksum_pseudo_header, in_cksum_skip, in_pseudo, init, ipv4_finalize,
                   ipv4_verify, ipv4_verify_multi, ipv4_verify_host, rx_offload_host, ipv4_verify_repeat, VerifyRepeat, rx_offload, set_busy_wait, set_shape, set_run_kernel, verify_plan, span_batch, synth_ipv4, version,
-                  TxBatch, tx_copy, tx_copy_host, page_buffer, set_dropin_mode, dropin_degraded)
+                  TxBatch, TxRepeat, tx_copy, tx_copy_host, page_buffer, set_dropin_mode, dropin_degraded)
 
 load()
 
@@ -19,5 +19,5 @@ __all__ = [
     "MiCksumError", "load", "ChainBatch", "MbufChain", "chain_batch", "PktBatch", "device_count", "host_register", "host_unregister",
     "in_addword", "in_cksum", "in_cksum_hdr", "in_cksum_pseudo_header", "in_cksum_skip", "in_pseudo", "init",
     "ipv4_finalize", "ipv4_verify", "ipv4_verify_multi", "ipv4_verify_host", "rx_offload_host", "ipv4_verify_repeat", "VerifyRepeat", "rx_offload", "set_busy_wait", "span_batch", "verify_plan", "synth_ipv4", "version",
-    "TxBatch", "tx_copy", "tx_copy_host", "page_buffer", "set_dropin_mode", "dropin_degraded",
+    "TxBatch", "TxRepeat", "tx_copy", "tx_copy_host", "page_buffer", "set_dropin_mode", "dropin_degraded",
 ]

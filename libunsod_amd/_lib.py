@@ -142,6 +142,8 @@ SIGNATURES = {
                                              C.c_void_p]),
     "mi_cksum_tx_copy": (C.c_int, [C.POINTER(TxBatchC), C.c_void_p, C.c_void_p]),
     "mi_cksum_tx_copy_host": (C.c_int, [C.POINTER(TxBatchC), C.c_void_p, C.c_uint32]),
+    "mi_cksum_tx_repeat_create": (C.c_int, [C.POINTER(TxBatchC), C.c_uint32, C.POINTER(C.c_void_p), C.c_uint32,
+                                            C.POINTER(C.c_void_p)]),
     "mi_cksum_verify_plan": (C.c_char_p, [C.POINTER(PktBatchC)]),
     "mi_cksum_rx_offload": (C.c_int, [C.POINTER(PktBatchC), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "mi_cksum_ipv4_verify_repeat": (C.c_int, [C.POINTER(PktBatchC), C.c_uint32, C.POINTER(C.c_void_p),

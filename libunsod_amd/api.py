@@ -449,6 +449,34 @@ class VerifyRepeat:
             pass
 
 
+class TxRepeat(VerifyRepeat):
+    """A prepared back-to-back fused-TX submission (mi_cksum_tx_repeat_create):
+    pass k copies batches[k % nb] (TxBatch) with its sums into its slots and
+    its per-frame status into statuses[k % nb] (device uint8, n each), on the
+    handle's streams.  ``engine="aql"``: prebuilt AQL packets of the default
+    TX kernel instead of HIP launches.  ``run`` / ``span`` / ``close`` as for
+    VerifyRepeat."""
+
+    def __init__(self, batches, statuses, nstreams: int = 2, engine: str = "hip"):
+        nb = len(batches)
+        if len(statuses) != nb:
+            raise ValueError("one status array per batch")
+        self._keep = (batches, statuses)
+        arr = (TxBatchC * nb)(*[b.c for b in batches])
+        VP = C.c_void_p * nb
+        st = VP(*[_ptr(s) for s in statuses])
+        h = C.c_void_p()
+        lib = load()
+        check("mi_cksum_tx_repeat_create", lib.mi_cksum_tx_repeat_create(arr, nb, st, nstreams, C.byref(h)))
+        self._h = h
+        self.engine = engine
+        if engine != "hip":
+            check("mi_cksum_repeat_set_engine", lib.mi_cksum_repeat_set_engine(h, {"aql": 1}[engine]))
+        self._run = lib.mi_cksum_repeat_run
+        self._span = C.c_float(0.0)
+        self._span_ref = C.byref(self._span)
+
+
 def synth_ipv4(b: PktBatch, seed: int = 0x5EED5EED, stream=None) -> None:
     """Device-side workload generator (not part of the reference API)."""
     check("mi_cksum_synth_ipv4", load().mi_cksum_synth_ipv4(C.byref(b.c), seed, C.c_void_p(_stream(stream))))

@@ -1494,6 +1494,11 @@ extern "C" __global__ __launch_bounds__(kBlock) void mi_aql_slot64(Desc d, uint1
                                                                    uint32_t *bad) {
   slot64_body(d, ip, l4, st, bad);
 }
+// (the fused TX copy's default kernel, k_tx_lds<2, MI_TX_LDS_R>: one argument,
+// the TxDesc; the repeat handle of mi_cksum_tx_repeat_create)
+extern "C" __global__ __launch_bounds__(64, tx_lds_waves(2, MI_TX_LDS_R)) void mi_aql_tx_lds(TxDesc t) {
+  tx_lds_body<2, MI_TX_LDS_R, false>(t);
+}
 namespace {
 // The 100 MHz constant clock (the clock of the queues' dispatch timestamps).
 __device__ __forceinline__ uint64_t rt_clock() {
@@ -2770,6 +2775,15 @@ int tx_kernel_kind() {
 // The 8x2 lane-group kernel with the next pass's loads issued before this
 // pass's stores (k_tx_copy EL): MI_CKSUM_TX_EARLY=1 / 0, read
 // per call (A/B in one process); unset: the build default MI_TX_EARLY_LOADS.
+// Whether launch_tx runs the default LDS kernel (what the AQL engine's
+// mi_aql_tx_lds is): no kernel, shape or ring override in force.
+bool tx_default_lds() {
+  if (tx_kernel_kind() != 3 || tx_shape_forced()) return false;
+  const char *e = getenv("MI_CKSUM_TX_LDS");
+  int u = 2, r = MI_TX_LDS_R;
+  if (e && sscanf(e, "%dx%d", &u, &r) < 1) return false;
+  return u == 2 && r == MI_TX_LDS_R && !(e && strchr(e, 'c'));
+}
 bool tx_early_loads() {
   const char *e = getenv("MI_CKSUM_TX_EARLY");
   return e ? e[0] == '1' : MI_TX_EARLY_LOADS != 0;
@@ -2793,7 +2807,7 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
   if (tx_kernel_kind() == 3 && !tx_shape_forced()) {
     // the LDS-staged gather: one wave (8 frames) per workgroup, the same total
     // waves as k_tx_copy's grid
-    const unsigned grid = (unsigned)std::min<uint64_t>(((uint64_t)t.n + 7u) / 8u, 4ull * grid_for(t.n, 8));
+    const unsigned grid = tx_lds_grid(t.n, (unsigned)grid_for(t.n, 8));
     // MI_CKSUM_TX_LDS = "UxR": chunks per lane per pass, ring depth (read per
     // call: A/B in one process); default 2 x MI_TX_LDS_R
     int u = 2, r = MI_TX_LDS_R;
@@ -2859,7 +2873,7 @@ enum AqlKernelId {
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
-  kAqlSlot64, kAqlScalar, kAqlSvc, kAqlSpin, kAqlKernels
+  kAqlSlot64, kAqlTx, kAqlScalar, kAqlSvc, kAqlSpin, kAqlKernels
 };
 const char *const kAqlNames[kAqlKernels] = {
 #define X(G_, U_) "mi_aql_v_" #G_ "x" #U_,
@@ -2873,7 +2887,7 @@ const char *const kAqlNames[kAqlKernels] = {
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    "mi_aql_slot64", "mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin"};
+    "mi_aql_slot64", "mi_aql_tx_lds", "mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin"};
 const void *const kAqlFuncs[kAqlKernels] = {
 #define X(G_, U_) (const void *)mi_aql_v_##G_##x##U_,
     MI_AQL_SHAPES(X)
@@ -2888,7 +2902,8 @@ const void *const kAqlFuncs[kAqlKernels] = {
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
-    (const void *)mi_aql_slot64, (const void *)mi_aql_scalar, (const void *)mi_aql_dropin_svc, (const void *)mi_aql_spin};
+    (const void *)mi_aql_slot64, (const void *)mi_aql_tx_lds, (const void *)mi_aql_scalar,
+    (const void *)mi_aql_dropin_svc, (const void *)mi_aql_spin};
 
 // The kernels' explicit arguments, laid out as the compiler lays out the
 // kernel-argument segment (each parameter at its natural alignment).  The
@@ -2906,6 +2921,7 @@ struct AqlDealArgs {  // mi_aql_vd_*: the verify arguments and the counter set
 };
 bool aql_is_deal(int id) { return id >= kAqlVD_1x4 && id <= kAqlVD_8x12; }
 constexpr uint32_t kAqlHidden = (sizeof(AqlArgs) + 7u) & ~7u;
+constexpr uint32_t kAqlTxHidden = (sizeof(TxDesc) + 7u) & ~7u;  // mi_aql_tx_lds
 
 struct AqlKernel {
   uint64_t object = 0;
@@ -3156,10 +3172,11 @@ int aql_device(int dev, AqlDevice **out) {
       for (int i = 0; i < kAqlKernels && !a.rc; ++i) {
         if (!a.k[i].object) fail(-ENOENT, "kernel %s not found in the loaded code objects", kAqlNames[i]);
         else if (a.k[i].kernarg < (i == kAqlScalar ? 56u : i == kAqlSvc ? 32u : i == kAqlSpin ? 8u
+                                   : i == kAqlTx ? kAqlTxHidden + 66u
                                    : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) + 66u : kAqlHidden + 66u) ||
                  a.k[i].kernarg > 512u)
           fail(-EPROTO, "%s: kernarg segment %u B (explicit arguments %u B)", kAqlNames[i], a.k[i].kernarg,
-               i == kAqlScalar ? 56u : i == kAqlSvc ? 32u : i == kAqlSpin ? 8u
+               i == kAqlScalar ? 56u : i == kAqlSvc ? 32u : i == kAqlSpin ? 8u : i == kAqlTx ? (unsigned)sizeof(TxDesc)
                : aql_is_deal(i) ? (unsigned)sizeof(AqlDealArgs) : (unsigned)sizeof(AqlArgs));
       }
     }
@@ -3331,6 +3348,7 @@ unsigned aql_wg(int id) {
     case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: case kAqlRun4w2o: case kAqlRun8w2o:
       return 128;
     case kAqlScalar: return kScalarThreads;
+    case kAqlTx: return 64;
     default: return kBlock;
   }
 }
@@ -3355,6 +3373,7 @@ void aql_fill_packet(hsa_kernel_dispatch_packet_t &p, const AqlKernel &k, unsign
   p.kernarg_address = kargs;
 }
 
+int aql_open(AqlRun *a);
 // Build the engine for nb batches: kernel-argument blocks (device memory,
 // written once) and one dispatch packet template per batch.
 int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *const *ip, uint16_t *const *l4,
@@ -3419,15 +3438,23 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     aql_free(a);
     return set_err(-EIO, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
   }
+  if ((rc = aql_open(a))) return rc;
+  *out = a;
+  return 0;
+}
+
+// The run's HSA queues and completion signals (on failure a is freed).
+int aql_open(AqlRun *a) {
+  int rc = 0;
   {
     // (placement: the drop-in queues, created later, avoid these classes)
     std::lock_guard<std::mutex> lk(g_qplace_mu);
     for (uint32_t q = 0; q < a->nq; ++q) {
-      if ((rc = aql_queue_create(dv->agent, 4096, &a->err, &a->q[q]))) {
+      if ((rc = aql_queue_create(a->dev->agent, 4096, &a->err, &a->q[q]))) {
         aql_free(a);
         return rc;
       }
-      ++dv->batch_cnt[a->q[q]->id % kPipes];
+      ++a->dev->batch_cnt[a->q[q]->id % kPipes];
       (void)hsa_amd_profiling_set_profiler_enabled(a->q[q], 1);
     }
   }
@@ -3441,6 +3468,46 @@ int aql_create(int device, const Desc *d, const uint32_t *max_len, uint16_t *con
     return set_err(-EIO, "AQL engine: hsa_signal_create failed");
   }
   a->have_rest = true;
+  return 0;
+}
+
+// The engine for nb fused-TX batches (mi_cksum_tx_repeat_create): the default
+// TX kernel (k_tx_lds<2, MI_TX_LDS_R>) as mi_aql_tx_lds, the TxDesc as its
+// one argument, the grid launch_tx gives it.
+int aql_create_tx(int device, const TxDesc *t, uint32_t nb, uint32_t nqueues, AqlRun **out) {
+  AqlDevice *dv = nullptr;
+  int rc = aql_device(device, &dv);
+  if (rc) return rc;
+  AqlRun *a = new AqlRun();
+  a->dev = dv;
+  a->nq = std::min(std::max(nqueues, 1u), 4u);
+  const uint32_t nq = a->nq;
+  const uint32_t slot = (dv->k[kAqlTx].kernarg + 63u) & ~63u;
+  std::vector<uint8_t> host((size_t)slot * nb * nq, 0);
+  a->pkt.resize((size_t)nb * nq);
+  hipError_t e = jmalloc((void **)&a->kargs, host.size());
+  a->kargs_bytes = host.size();
+  jnote("aql tx kargs", a->kargs, host.size(), nb);
+  if (e != hipSuccess) {
+    aql_free(a);
+    return set_err(-ENOMEM, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
+  }
+  for (uint32_t j = 0; j < nb; ++j) {
+    const unsigned blocks = tx_lds_grid(t[j].n, (unsigned)grid_for(t[j].n, 8));
+    for (uint32_t q = 0; q < nq; ++q) {
+      const size_t k = (size_t)j * nq + q;
+      aql_fill_raw(host.data() + slot * k, &t[j], sizeof(TxDesc), blocks, aql_wg(kAqlTx), dv->k[kAqlTx].kernarg);
+      aql_fill_packet(a->pkt[k], dv->k[kAqlTx], blocks, a->kargs + slot * k, aql_wg(kAqlTx));
+    }
+    jnote("  aql tx src", t[j].src, t[j].src_bytes, t[j].n);
+    jnote("  aql tx dst", t[j].dst, t[j].dst_bytes);
+  }
+  e = hipMemcpy(a->kargs, host.data(), host.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    aql_free(a);
+    return set_err(-EIO, "AQL engine: kernel arguments: %s", hipGetErrorString(e));
+  }
+  if ((rc = aql_open(a))) return rc;
   *out = a;
   return 0;
 }
@@ -4533,6 +4600,7 @@ struct mi_repeat {
   uint32_t seq = 0;
   double trace[8] = {};  // MI_CKSUM_REPEAT_TRACE: host timestamps of the last run (s)
   AqlRun *aql = nullptr;  // MI_REPEAT_ENGINE_AQL
+  std::vector<TxDesc> tx;  // MI_REPEAT_OP_TX_COPY (mi_cksum_tx_repeat_create): the batches
   uint32_t *deal = nullptr;  // dealt-unit counter sets, one per stream (the AQL engine has its own)
   uint32_t *deal_set(uint32_t q) const { return deal ? deal + q * (kDealSetBytes / 4u) : nullptr; }
 };
@@ -4679,7 +4747,7 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
   // Timing events ride on the launches themselves (hipExtLaunchKernel): ev0
   // starts with the first pass, ev_end[q] stops with stream q's last pass.
   // A length-class plan (several launches per pass) uses marker events.
-  const bool ext = timed && steps > 0 && repeat_ext_events() &&
+  const bool ext = timed && steps > 0 && repeat_ext_events() && r->op != MI_REPEAT_OP_TX_COPY &&
                    (r->op == MI_REPEAT_OP_FINALIZE ? finalize_uses_vlaunch(r->d[0])
                                                    : verify_plan(r->d[0], r->ml[0]).kind != kPlanClasses);
   if (timed && !ext) HIP_TRY(hipEventRecord(r->ev0, r->s[0]));
@@ -4691,7 +4759,9 @@ int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *spa
       t_lev.start = k == 0 ? r->ev0 : nullptr;
       t_lev.stop = k + ns >= steps ? r->ev_end[k % ns] : nullptr;
     }
-    if (r->op == MI_REPEAT_OP_FINALIZE)
+    if (r->op == MI_REPEAT_OP_TX_COPY)
+      rc = launch_tx(r->tx[j], pick_tx_shape(r->ml[j]), r->s[k % ns]);
+    else if (r->op == MI_REPEAT_OP_FINALIZE)
       rc = launch_finalize(r->d[j], pick_shape(r->ml[j]), r->s[k % ns], r->mlen[j]);
     else
       rc = launch_verify(r->d[j], r->ml[j], r->ip[j], r->l4[j], r->st[j], nullptr, r->s[k % ns], r->deal_set(k % ns));
@@ -4786,7 +4856,13 @@ int mi_cksum_repeat_set_engine(mi_repeat *r, uint32_t engine) {
     r->aql = nullptr;
   }
   if (engine == MI_REPEAT_ENGINE_HIP) return 0;
-  if (r->op != MI_REPEAT_OP_VERIFY) return set_err(-ENOTSUP, "AQL engine: verify passes only");
+  if (r->op == MI_REPEAT_OP_TX_COPY) {
+    if (!tx_default_lds())
+      return set_err(-ENOTSUP, "AQL engine: TX passes run the default kernel (k_tx_lds 2x%d) only", MI_TX_LDS_R);
+    for (uint32_t q = 0; q < r->nstreams; ++q) HIP_TRY(hipStreamSynchronize(r->s[q]));
+    return aql_create_tx(r->device, r->tx.data(), r->nb, r->nstreams, &r->aql);
+  }
+  if (r->op != MI_REPEAT_OP_VERIFY) return set_err(-ENOTSUP, "AQL engine: verify or TX-copy passes only");
   for (uint32_t q = 0; q < r->nstreams; ++q) HIP_TRY(hipStreamSynchronize(r->s[q]));
   return aql_create(r->device, r->d.data(), r->ml.data(), r->ip.data(), r->l4.data(), r->st.data(), r->nb,
                     r->nstreams, &r->aql);
@@ -4795,6 +4871,7 @@ int mi_cksum_repeat_set_engine(mi_repeat *r, uint32_t engine) {
 int mi_cksum_repeat_set_op(mi_repeat *r, uint32_t op) {
   if (!r) return set_err(-EINVAL, "handle is NULL");
   if (op != MI_REPEAT_OP_VERIFY && op != MI_REPEAT_OP_FINALIZE) return set_err(-EINVAL, "op %u", op);
+  if (r->op == MI_REPEAT_OP_TX_COPY) return set_err(-EINVAL, "a TX-copy handle runs TX-copy passes only");
   if (r->aql && op != MI_REPEAT_OP_VERIFY) return set_err(-ENOTSUP, "AQL engine: verify passes only");
   r->op = op;
   return 0;
@@ -4861,6 +4938,40 @@ int mi_cksum_tx_copy(const mi_tx_batch *b, uint8_t *status, void *stream) {
   TxDesc t;
   if ((rc = make_txdesc(b, status, &t))) return rc;
   return launch_tx(t, pick_tx_shape(b->max_len ? b->max_len : b->room), (hipStream_t)stream);
+}
+
+int mi_cksum_tx_repeat_create(const mi_tx_batch *b, uint32_t nb, uint8_t *const *status, uint32_t nstreams,
+                              mi_repeat **out) {
+  int rc = ensure_ctx();
+  if (rc) return rc;
+  if (!out) return set_err(-EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!b || !nb || !status) return set_err(-EINVAL, "no batches");
+  if (nb > 1024) return set_err(-EINVAL, "at most 1024 batches");
+  if (nstreams < 1 || nstreams > ThreadCtx::kMaxRep) return set_err(-EINVAL, "nstreams 1..%d", ThreadCtx::kMaxRep);
+  std::vector<TxDesc> tx(nb);
+  for (uint32_t k = 0; k < nb; ++k) {
+    if (!b[k].n) return set_err(-EINVAL, "batch %u is empty", k);
+    if ((rc = make_txdesc(&b[k], status[k], &tx[k]))) return rc;
+  }
+  // the stream / event set of a verify handle, then the TX batches in place
+  // of its descriptors
+  mi_repeat *r = nullptr;
+  {
+    std::vector<mi_pkt_batch> none(nb);
+    for (auto &p : none) {
+      memset(&p, 0, sizeof p);
+      p.base = b[0].dst;  // (any valid pointer: n = 0, nothing is read)
+      p.bytes = 16;
+      p.stride = 16;
+    }
+    if ((rc = mi_cksum_repeat_create(none.data(), nb, nullptr, nullptr, nullptr, nstreams, &r))) return rc;
+  }
+  r->op = MI_REPEAT_OP_TX_COPY;
+  r->tx = std::move(tx);
+  for (uint32_t k = 0; k < nb; ++k) r->ml[k] = b[k].max_len ? b[k].max_len : b[k].room;
+  *out = r;
+  return 0;
 }
 
 int mi_cksum_ipv4_finalize(const mi_pkt_batch *b, void *stream) {

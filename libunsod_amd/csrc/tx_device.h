@@ -1075,8 +1075,9 @@ __device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
   c.slow = k & 128u;
   return c;
 }
-template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false>
-__global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
+// (the body, shared by k_tx_lds and the AQL engine's mi_aql_tx_lds)
+template <int U, int R, bool CC>
+__device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
   constexpr int G = 8;
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
@@ -1293,6 +1294,16 @@ __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
     prefetch2();
     if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
   }
+}
+template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false>
+__global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
+  tx_lds_body<U, R, CC>(t);
+}
+// Its grid: one wave (8 frames) per workgroup, the same total waves as
+// k_tx_copy's 8 x 2 grid at the default cap.
+inline unsigned tx_lds_grid(uint32_t n, unsigned copy_blocks) {
+  const uint64_t g = std::min<uint64_t>(((uint64_t)n + 7u) / 8u, 4ull * copy_blocks);
+  return g ? (unsigned)g : 1u;
 }
 
 #endif  // MI_TX_DEVICE_H

@@ -51,9 +51,18 @@ def _kernels(tmp_path):
 
 def test_aql_entry_points_kernarg_layout(tmp_path):
     ks = _kernels(tmp_path)
-    verify = [k for k in ks if k not in ("mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin")]
+    verify = [k for k in ks if k not in ("mi_aql_scalar", "mi_aql_dropin_svc", "mi_aql_spin", "mi_aql_tx_lds")]
     assert "mi_aql_v_16x6" in ks and "mi_aql_run8" in ks and "mi_aql_slot64" in ks and "mi_aql_scalar" in ks
-    assert "mi_aql_vd_16x6" in ks and "mi_aql_vd_8x12" in ks
+    assert "mi_aql_vd_16x6" in ks and "mi_aql_vd_8x12" in ks and "mi_aql_tx_lds" in ks
+    # mi_aql_tx_lds(TxDesc): one 120-byte by-value argument, the hidden block
+    # right after it (aql_create_tx writes sizeof(TxDesc) bytes, then kAqlTxHidden)
+    args, seg = ks["mi_aql_tx_lds"]
+    explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]
+    assert explicit == [(0, 120)], explicit
+    for o, s, k in args:
+        if k in HIDDEN:
+            assert o == 120 + HIDDEN[k], ("mi_aql_tx_lds", k, o)
+    assert seg <= 512, seg
     for name in verify:
         args, seg = ks[name]
         explicit = [(o, s) for o, s, k in args if not k.startswith("hidden_")]

@@ -162,3 +162,78 @@ def test_tx_lds_many_frames_per_wave():
             assert bad.size == 0, (name, bad.size, bad[:8])
     finally:
         mi.set_shape(0, 0, 0)
+
+
+def _tx_batch(c):
+    src = torch.from_numpy(c["src"]).cuda()
+    dst = torch.from_numpy(c["dst"].copy()).cuda()
+    tb = mi.TxBatch(src, c["seg_off"], c["seg_len"], c["pkt_seg"], c["pkt_len"], dst, dst_stride=c["stride"],
+                    dst_first=c["dst_first"], room=c["room"], l3_off=c["l3"], csum_flags=c["flags"],
+                    csum_data=c["data"], max_len=int(c["pkt_len"].max()))
+    st = torch.full((tb.n,), 0xEE, dtype=torch.uint8, device="cuda")
+    return tb, st
+
+
+@pytest.mark.parametrize("engine", ["hip", "aql"])
+def test_tx_repeat_every_case(engine):
+    """The prepared TX handle (mi_cksum_tx_repeat_create; the bench's TX leg)
+    through HIP launches and as AQL packets of mi_aql_tx_lds: every edge case,
+    two batches per handle rotating over five passes on two queues, each
+    batch's slots and status byte for byte against the oracle."""
+    cases = [(n, c) for n, c in CASES if c["pkt_len"].size]
+    for k in range(0, len(cases), 2):
+        pair = cases[k:k + 2]
+        made = [_tx_batch(c) for _, c in pair]
+        torch.cuda.synchronize()
+        rep = mi.TxRepeat([tb for tb, _ in made], [st for _, st in made], nstreams=2, engine=engine)
+        try:
+            rep.run(5, timed=True)
+            assert rep.span() > 0
+        finally:
+            rep.close()
+        for (name, c), (tb, st) in zip(pair, made):
+            want_dst, want_st = run_oracle(ORC, c)
+            got_st = st.cpu().numpy()
+            assert np.array_equal(got_st, want_st), (engine, name, np.nonzero(got_st != want_st)[0][:8])
+            bad = np.nonzero(tb.dst.cpu().numpy() != want_dst)[0]
+            assert bad.size == 0, (engine, name, bad.size, bad[:8])
+
+
+def test_tx_repeat_full_size_aql_equals_launch():
+    """65536 x 1514 B socket chains, three batches rotating over 7 passes of
+    the AQL engine: the slots and status equal mi_cksum_tx_copy's and the
+    oracle's."""
+    c = make_case(65536, 1500, layout="socket", seed=33)
+    want_dst, want_st = run_oracle(ORC, c)
+    made = [_tx_batch(c) for _ in range(3)]
+    torch.cuda.synchronize()
+    rep = mi.TxRepeat([tb for tb, _ in made], [st for _, st in made], nstreams=2, engine="aql")
+    try:
+        rep.run(7, timed=True)
+        us = rep.span() / 7
+    finally:
+        rep.close()
+    assert us > 0
+    for tb, st in made:
+        assert np.array_equal(st.cpu().numpy(), want_st)
+        assert np.array_equal(tb.dst.cpu().numpy(), want_dst)
+
+
+def test_tx_repeat_aql_needs_the_default_kernel(monkeypatch):
+    """The AQL engine carries the default TX kernel only: with another ring
+    selected it refuses (-ENOTSUP) instead of running something else; HIP
+    launches still honour the override."""
+    c = dict(CASES)["socket-1514"]
+    tb, st = _tx_batch(c)
+    torch.cuda.synchronize()
+    monkeypatch.setenv("MI_CKSUM_TX_LDS", "2x3")
+    with pytest.raises(mi.MiCksumError):
+        mi.TxRepeat([tb], [st], engine="aql")
+    rep = mi.TxRepeat([tb], [st], engine="hip")
+    try:
+        rep.run(2)
+    finally:
+        rep.close()
+    want_dst, want_st = run_oracle(ORC, c)
+    assert np.array_equal(st.cpu().numpy(), want_st)
+    assert np.array_equal(tb.dst.cpu().numpy(), want_dst)
