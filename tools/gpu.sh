@@ -45,9 +45,11 @@ for step in "$@"; do
       tail -1 "$O/smoke.log" ;;
     bench)
       cfg=${a:-1500}
+      sfx=$(echo "$extra" | tr -c 'A-Za-z0-9\n' '_' | sed 's/^_*//')  # one file per (config, flags)
+      bj="$O/bench_$cfg${sfx:+_$sfx}"
       timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --config "$cfg" $extra \
-        > "$O/bench_$cfg.json" 2> "$O/bench_$cfg.err" || fail "$step" $?
-      cut -c1-400 "$O/bench_$cfg.json" ;;
+        > "$bj.json" 2> "$bj.err" || fail "$step" $?
+      cut -c1-400 "$bj.json" ;;
     bench400)
       cfg=${a:-1500}
       timeout -k 10 300 python -u bench.py --gpus 1 --steps 400 --warmup 5 --config "$cfg" --also none \
