@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--saux", default="0,1,2,3", help="comma list of store policies")
     ap.add_argument("--geom", default="slots,dense")
     ap.add_argument("--soff", default="0,6")
+    ap.add_argument("--torch-copy", dest="torch_copy", default="torch", help="'torch': also time torch copy_; '' skips")
     a = ap.parse_args()
     torch.cuda.set_device(0)
     lib = C.CDLL(os.path.join(ROOT, "tools", "libceiling.so"))
@@ -64,6 +65,37 @@ def main():
                                               src_misalign=soff, store_aux=saux, unroll=unroll, grid=grid, R=R,
                                               us_per_launch=round(us, 3), frac_of_8TBps=round(alg / us / 8e6, 4))),
                               flush=True)
+
+    if "torch" in a.torch_copy:
+        # the runtime's own device-to-device copy of the same byte count
+        # (n frames back to back, no slots): torch copy_ over rotating buffers
+        # alternating over two streams, span from events on those streams
+        nb = n * fr
+        tsrc = [t[:nb] for t in srcs]
+        tdst = [t[:nb] for t in dsts]
+        streams = [torch.cuda.Stream() for _ in range(2)]
+
+        def run(k):
+            for j in range(k):
+                with torch.cuda.stream(streams[j % 2]):
+                    tdst[j % R].copy_(tsrc[j % R])
+        run(100)
+        torch.cuda.synchronize()
+        e0 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+        e1 = [torch.cuda.Event(enable_timing=True) for _ in streams]
+        g = torch.cuda.Event()
+        g.record(streams[0])
+        streams[1].wait_event(g)
+        for e, s_ in zip(e0, streams):
+            e.record(s_)
+        run(a.steps)
+        for e, s_ in zip(e1, streams):
+            e.record(s_)
+        torch.cuda.synchronize()
+        us = max(e0[0].elapsed_time(e) for e in e1) * 1e3 / a.steps
+        print(json.dumps(dict(probe="torch copy_ (dense D2D)", bytes=nb, R=R, us_per_launch=round(us, 3),
+                              frac_of_8TBps=round(n * (2 * fr + 1) / us / 8e6, 4))), flush=True)
+
 
 if __name__ == "__main__":
     main()
