@@ -4649,6 +4649,7 @@ bool repeat_ext_events() {
   }();
   return on;
 }
+int repeat_open(mi_repeat *r, uint32_t nb, uint32_t nstreams);
 bool repeat_trace_on() {
   static const bool on = getenv("MI_CKSUM_REPEAT_TRACE") != nullptr;
   return on;
@@ -4672,9 +4673,6 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
   if (nb > 1024) return set_err(-EINVAL, "at most 1024 batches");
   if (nstreams < 1 || nstreams > ThreadCtx::kMaxRep) return set_err(-EINVAL, "nstreams 1..%d", ThreadCtx::kMaxRep);
   mi_repeat *r = new mi_repeat();
-  r->device = t_ctx.device;
-  r->nb = nb;
-  r->nstreams = nstreams;
   r->d.resize(nb);
   r->ml.resize(nb);
   r->ip.resize(nb);
@@ -4691,6 +4689,19 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
     r->l4[k] = l4 ? l4[k] : nullptr;
     r->st[k] = status ? status[k] : nullptr;
   }
+  if ((rc = repeat_open(r, nb, nstreams))) return rc;
+  *out = r;
+  return 0;
+}
+
+}  // extern "C"
+
+namespace {
+// The handle's streams, events and counters (on failure r is freed).
+int repeat_open(mi_repeat *r, uint32_t nb, uint32_t nstreams) {
+  r->device = t_ctx.device;
+  r->nb = nb;
+  r->nstreams = nstreams;
   hipError_t e = hipSuccess;
   for (uint32_t q = 0; q < nstreams && e == hipSuccess; ++q) {
     e = hipStreamCreateWithFlags(&r->s[q], hipStreamNonBlocking);
@@ -4711,9 +4722,11 @@ int mi_cksum_repeat_create(const mi_pkt_batch *b, uint32_t nb, uint16_t *const *
     repeat_free(r);
     return set_err(-EIO, "repeat_create: %s", hipGetErrorString(e));
   }
-  *out = r;
   return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int mi_cksum_repeat_run(mi_repeat *r, uint32_t steps, uint32_t flags, float *span_us) {
   if (!r) return set_err(-EINVAL, "handle is NULL");
@@ -4954,22 +4967,12 @@ int mi_cksum_tx_repeat_create(const mi_tx_batch *b, uint32_t nb, uint8_t *const 
     if (!b[k].n) return set_err(-EINVAL, "batch %u is empty", k);
     if ((rc = make_txdesc(&b[k], status[k], &tx[k]))) return rc;
   }
-  // the stream / event set of a verify handle, then the TX batches in place
-  // of its descriptors
-  mi_repeat *r = nullptr;
-  {
-    std::vector<mi_pkt_batch> none(nb);
-    for (auto &p : none) {
-      memset(&p, 0, sizeof p);
-      p.base = b[0].dst;  // (any valid pointer: n = 0, nothing is read)
-      p.bytes = 16;
-      p.stride = 16;
-    }
-    if ((rc = mi_cksum_repeat_create(none.data(), nb, nullptr, nullptr, nullptr, nstreams, &r))) return rc;
-  }
+  mi_repeat *r = new mi_repeat();
   r->op = MI_REPEAT_OP_TX_COPY;
   r->tx = std::move(tx);
+  r->ml.resize(nb);
   for (uint32_t k = 0; k < nb; ++k) r->ml[k] = b[k].max_len ? b[k].max_len : b[k].room;
+  if ((rc = repeat_open(r, nb, nstreams))) return rc;
   *out = r;
   return 0;
 }

@@ -35,6 +35,12 @@ VARIANTS = {
     # 4-wave workgroups' worth, i.e. 4 cap one-wave workgroups; 2048 = default)
     "lds2x2c1024": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2", _cap=1024),
     "lds2x2c1536": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2", _cap=1536),
+    # the wave-per-frame kernel (k_tx_wave<2>, 4 waves per workgroup) at larger
+    # grids: 16384 workgroups = one frame per wave, one-shot
+    "wave": dict(MI_CKSUM_TX_KERNEL="wave"),
+    "wave4k": dict(MI_CKSUM_TX_KERNEL="wave", _cap=4096),
+    "wave8k": dict(MI_CKSUM_TX_KERNEL="wave", _cap=8192),
+    "wave16k": dict(MI_CKSUM_TX_KERNEL="wave", _cap=16384),
 }
 
 
