@@ -352,7 +352,8 @@ def measure(mi, shard, wl: dict, args, K: int, dev, dist, backend: str, sustain_
     # HBM bytes per launch from the newest PMC record of this config (request-
     # size counters, rounds 3-5; FETCH_SIZE x2, round 2), labelled with its source
     tkey = config + ("_u64" if args.offs64 else "_u32") if config == "pareto" else config
-    for rel in ("profiles/r05/pmc_traffic_r05.json", "profiles/r04/pmc_traffic_r04.json", "profiles/r03/pmc_traffic_r03.json",
+    for rel in ("profiles/r06/pmc_traffic_r06.json", "profiles/r05/pmc_traffic_r05.json", "profiles/r04/pmc_traffic_r04.json",
+                "profiles/r03/pmc_traffic_r03.json",
                 "profiles/pmc_traffic_r02.json"):
         tfile = os.path.join(ROOT, rel)
         try:

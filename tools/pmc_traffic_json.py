@@ -23,7 +23,7 @@ CONFIGS = {
     "1500": ("1500", "k_ipv4_verify<16, 6>", 65536 * 1500 + 5 * 65536),
     "9000": ("9000", "k_ipv4_verify<8, 12>", 65536 * 9000 + 5 * 65536),
     "64": ("64", "k_ipv4_verify_slot64", (1 << 20) * 46 + 5 * (1 << 20)),
-    "pareto": ("pareto_u32", "k_ipv4_verify_packed<8, 0, 2>", None),
+    "pareto": ("pareto_u32", "k_ipv4_verify_packed<8, 0, 2, false>", None),
     # bench.py config_tx: 65536 frames of 1514 B read + written + 1 B status
     "tx": ("tx", "k_tx_lds<2, 2>", 65536 * (2 * 1514 + 1)),
 }
