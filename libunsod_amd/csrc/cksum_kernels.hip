@@ -3255,6 +3255,17 @@ uint16_t aql_release_scope() {
   return sc;
 }
 
+// Acquire scope of each queue's first packet of a run (MI_CKSUM_AQL_ACQUIRE=
+// agent: diagnostics only -- the batches' producers may be DMA engines or
+// the host, whose writes a system-scope acquire makes visible).
+uint32_t aql_first_acquire_scope() {
+  static const uint32_t sc = [] {
+    const char *e = getenv("MI_CKSUM_AQL_ACQUIRE");
+    return (uint32_t)(e && !strcmp(e, "agent") ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM);
+  }();
+  return sc;
+}
+
 // Barrier bit of every packet (MI_CKSUM_AQL_BARRIER, default 1): each queue
 // runs its passes in order, like a HIP stream, and consecutive passes overlap
 // across queues.  With 0 a queue may start pass k+1 once pass k has dispatched
@@ -3580,7 +3591,7 @@ int aql_submit(AqlRun *a, uint32_t j0, uint32_t steps) {
     // -- DMA, the host, other queues -- may have rewritten them since the last
     // run; queues are not ordered after each other), later passes of the same
     // queue at agent scope (the barrier bit orders them after that acquire)
-    const uint32_t acq = k < a->nq ? HSA_FENCE_SCOPE_SYSTEM : HSA_FENCE_SCOPE_AGENT;
+    const uint32_t acq = k < a->nq ? aql_first_acquire_scope() : HSA_FENCE_SCOPE_AGENT;
     const uint32_t hs = (hdr_base | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE)) | ((uint32_t)t.setup << 16);
     __atomic_store_n((uint32_t *)slot, hs, __ATOMIC_RELEASE);
     last_idx[qi] = idx;
