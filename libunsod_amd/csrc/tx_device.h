@@ -1076,9 +1076,9 @@ __device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
   return c;
 }
 // (the body, shared by k_tx_lds and the AQL engine's mi_aql_tx_lds)
-template <int U, int R, bool CC>
+template <int U, int R, bool CC, int G = 8>
 __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
-  constexpr int G = 8;
+  static_assert(G == 8 || G == 16, "8 or 16 lanes per frame");
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
   __shared__ uint32_t s_seg[NG][kTxSeg][2];
@@ -1295,14 +1295,16 @@ __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
     if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
   }
 }
-template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false>
+template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false, int G = 8>
 __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
-  tx_lds_body<U, R, CC>(t);
+  tx_lds_body<U, R, CC, G>(t);
 }
-// Its grid: one wave (8 frames) per workgroup, the same total waves as
-// k_tx_copy's 8 x 2 grid at the default cap.
-inline unsigned tx_lds_grid(uint32_t n, unsigned copy_blocks) {
-  const uint64_t g = std::min<uint64_t>(((uint64_t)n + 7u) / 8u, 4ull * copy_blocks);
+// Its grid: one wave (64 / G frames) per workgroup; for G = 8 the same total
+// waves as k_tx_copy's 8 x 2 grid at the default cap (one frame group per
+// wave at the bench's 65536 frames), for G = 16 twice as many.
+inline unsigned tx_lds_grid(uint32_t n, unsigned copy_blocks, int G = 8) {
+  const uint64_t ng = 64u / (unsigned)G;
+  const uint64_t g = std::min<uint64_t>(((uint64_t)n + ng - 1u) / ng, 4ull * copy_blocks * (uint64_t)(G / 8));
   return g ? (unsigned)g : 1u;
 }
 
