@@ -1078,7 +1078,7 @@ __device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
 // (the body, shared by k_tx_lds and the AQL engine's mi_aql_tx_lds)
 template <int U, int R, bool CC, int G = 8>
 __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
-  static_assert(G == 8 || G == 16, "8 or 16 lanes per frame");
+  static_assert(G == 4 || G == 8 || G == 16, "4, 8 or 16 lanes per frame");
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
   __shared__ uint32_t s_seg[NG][kTxSeg][2];
@@ -1304,7 +1304,7 @@ __global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
 // wave at the bench's 65536 frames), for G = 16 twice as many.
 inline unsigned tx_lds_grid(uint32_t n, unsigned copy_blocks, int G = 8) {
   const uint64_t ng = 64u / (unsigned)G;
-  const uint64_t g = std::min<uint64_t>(((uint64_t)n + ng - 1u) / ng, 4ull * copy_blocks * (uint64_t)(G / 8));
+  const uint64_t g = std::min<uint64_t>(((uint64_t)n + ng - 1u) / ng, 4ull * copy_blocks * (uint64_t)G / 8u);
   return g ? (unsigned)g : 1u;
 }
 
