@@ -1230,6 +1230,12 @@ __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
         issue(p + R);  // the slot's reads have returned (lgkmcnt(0) in tx_ring_read)
         if (p == 0) {
           prefetch2();
+          if constexpr (G < 8) {  // the IPv4 header's first 20 bytes outside the held window: generic path
+            if (h + l3 + 20u > 16u * G) {
+              brk = true;
+              break;
+            }
+          }
           const u32x4 hv[1] = {v[0]};
           ih = parse_ipv4<G, 1>(hv, h + l3);
           const TxPlan pl = tx_plan(t, i, len, ih);
