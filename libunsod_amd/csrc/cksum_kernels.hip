@@ -2812,15 +2812,9 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
     // call: A/B in one process); default 2 x MI_TX_LDS_R
     int u = 2, r = MI_TX_LDS_R;
     if (const char *e = getenv("MI_CKSUM_TX_LDS")) (void)sscanf(e, "%dx%d", &u, &r);
-    // 16 lanes per frame (4 frames per wave, twice the waves): "2x2g16";
-    // 4 lanes per frame (16 frames per wave, half the waves): "2x2g4"
+    // 16 lanes per frame (4 frames per wave, twice the waves): "2x2g16"
     if (const char *e = getenv("MI_CKSUM_TX_LDS"); e && u == 2 && r == 2 && strstr(e, "g16")) {
       hipLaunchKernelGGL((k_tx_lds<2, 2, tx_lds_waves(2, 2), false, 16>), dim3(tx_lds_grid(t.n, (unsigned)grid_for(t.n, 8), 16)),
-                         dim3(64), 0, s, t);
-      return launched();
-    }
-    if (const char *e = getenv("MI_CKSUM_TX_LDS"); e && u == 2 && r == 2 && strstr(e, "g4")) {
-      hipLaunchKernelGGL((k_tx_lds<2, 2, tx_lds_waves(2, 2), false, 4>), dim3(tx_lds_grid(t.n, (unsigned)grid_for(t.n, 8), 4)),
                          dim3(64), 0, s, t);
       return launched();
     }

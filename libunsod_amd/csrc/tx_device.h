@@ -1078,7 +1078,7 @@ __device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
 // (the body, shared by k_tx_lds and the AQL engine's mi_aql_tx_lds)
 template <int U, int R, bool CC, int G = 8>
 __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
-  static_assert(G == 4 || G == 8 || G == 16, "4, 8 or 16 lanes per frame");
+  static_assert(G == 8 || G == 16, "8 or 16 lanes per frame (4: 0.38 of 8 TB/s, profiles/r06/tx_g4_ab_r06.jsonl)");
   constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
   __shared__ uint32_t s_seg[NG][kTxSeg][2];
@@ -1230,12 +1230,6 @@ __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
         issue(p + R);  // the slot's reads have returned (lgkmcnt(0) in tx_ring_read)
         if (p == 0) {
           prefetch2();
-          if constexpr (G < 8) {  // the IPv4 header's first 20 bytes outside the held window: generic path
-            if (h + l3 + 20u > 16u * G) {
-              brk = true;
-              break;
-            }
-          }
           const u32x4 hv[1] = {v[0]};
           ih = parse_ipv4<G, 1>(hv, h + l3);
           const TxPlan pl = tx_plan(t, i, len, ih);
