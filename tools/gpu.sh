@@ -20,6 +20,7 @@
 #   pmcpy:SCRIPT:C1,C2,..[:ARGS]  one rocprofv3 --pmc pass over python tools/SCRIPT
 #   host                  the box's identity (hostname, GPU serial, driver, clocks)
 #   rehearse2             the driver's N = 2 bench command, two ranks on device 0 over gloo
+#   rehearse:N            the same with N ranks (N <= 8)
 #
 #   /usr/local/graft/bin/gpurun --timeout 900 -- 'TAG=r03x bash tools/gpu.sh tests smoke bench bench:9000'
 set -o pipefail
@@ -83,14 +84,16 @@ for step in "$@"; do
       timeout -s KILL 180 rocprofv3 --pmc ${b//,/ } -d "$O/pmc_${scr}_$tag" -o run --output-format csv -- \
         python3 "tools/$scr.py" ${c//+/ } > "$O/pmc_${scr}_$tag.out" 2> "$O/pmc_${scr}_$tag.err" || fail "$step" $?
       echo "pmc $scr $b done" ;;
-    rehearse2)
-      # the driver's N = 2 command, both ranks on device 0 over gloo (RCCL
-      # refuses two ranks on one device): bench.py's N > 1 path end to end
+    rehearse2|rehearse)
+      # the driver's N-rank command (rehearse2: N = 2; rehearse:N), all ranks
+      # on device 0 over gloo (RCCL refuses two ranks on one device):
+      # bench.py's N > 1 path end to end
+      nr=2; [ "$kind" = rehearse ] && nr=${a:-2}
       MI_BENCH_DEVICE=0 MI_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
-        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 \
+        --nproc-per-node "$nr" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$nr" --steps 20 --warmup 5 \
         --cpu-seconds 0 --no-host-path --no-dropin --sustain-seconds 0 $extra \
-        > "$O/bench_n2_rehearsal.json" 2> "$O/bench_n2_rehearsal.err" || fail "$step" $?
-      tail -c 400 "$O/bench_n2_rehearsal.json" ;;
+        > "$O/bench_n${nr}_rehearsal.json" 2> "$O/bench_n${nr}_rehearsal.err" || fail "$step" $?
+      tail -c 400 "$O/bench_n${nr}_rehearsal.json" ;;
     host)
       { hostname; cat /sys/class/drm/card*/device/serial_number 2>/dev/null | head -8; rocm-smi --showproductname \
         --showserial --showmeminfo vram 2>/dev/null | grep -v "^$" | head -30; } > "$O/host.txt" 2>&1 || true
