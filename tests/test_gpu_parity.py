@@ -852,3 +852,68 @@ def test_repeat_handle_outputs_and_rotation():
     rep.run(1)
     rep.close()
     assert np.array_equal(cpu(buf), ref)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_verify_random_sweep(seed):
+    """Seeded random RX batches beyond the golden vectors: packet count,
+    lengths (uniform 20-9000 B or heavy-tailed), placement (fixed slots at a
+    random first offset, packed, shuffled, gappy), protocol and IP header
+    length per packet, then random single-byte corruptions and truncated
+    lengths.  ipv4_verify (and for every third seed the repeat handle's AQL
+    engine, for every fourth u32 offsets) against the oracle: ip / l4 /
+    status bit for bit."""
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.integers(1, 3000))
+    if rng.random() < 0.5:
+        lens = rng.integers(20, int(rng.choice([128, 1500, 9000])) + 1, n)
+    else:
+        lens = np.minimum(synth.pareto_lengths(n, seed=seed + 1), 9000)
+    lens = np.maximum(lens, 20).astype(np.int64)
+    proto = rng.choice([6, 17, 6, 17, 1], n)
+    hl = np.minimum(rng.choice([20, 20, 20, 24, 40, 60], n), lens & ~3)
+    layout = str(rng.choice(["slots", "packed", "shuffled", "gappy"]))
+    if layout == "slots":
+        stride = int(lens.max()) + int(rng.integers(0, 300))
+        first = int(rng.integers(0, 200))
+        b0 = synth.build_ipv4_batch(n, lens, stride=stride, first_off=first, seed=seed, proto=proto, hl=hl)
+        offs = (first + np.arange(n, dtype=np.int64) * stride).astype(np.uint64)
+    else:
+        offs = synth.packed_offsets(lens, first_off=int(rng.integers(0, 64)))
+        if layout == "gappy":
+            offs = offs + np.cumsum(rng.integers(0, 400, n)).astype(np.uint64)
+        b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=seed, proto=proto, hl=hl)
+    _, ref = aligned(b0["buf"])
+    ORC.ipv4_finalize_batch(ref, n, offs=offs, flen=lens.astype(np.uint32))
+    k = int(rng.integers(0, max(1, n // 10) + 1))
+    if k:
+        bad = rng.choice(n, k, replace=False)
+        at = offs[bad].astype(np.int64) + rng.integers(0, 1 << 30, k) % lens[bad]
+        ref[at] ^= rng.integers(1, 256, k).astype(np.uint8)
+    flen = lens.astype(np.uint32).copy()
+    cut = rng.choice(n, int(rng.integers(0, max(1, n // 20) + 1)), replace=False)
+    flen[cut] = rng.integers(0, 40, cut.size).astype(np.uint32) % np.maximum(flen[cut], 1)  # truncated frames
+    perm = rng.permutation(n) if layout == "shuffled" else np.arange(n)
+    o2, l2 = offs[perm], flen[perm]
+    ip_o, l4_o, st_o = ORC.ipv4_verify_batch(ref, n, offs=o2, flen=l2)
+    buf = dev_tensor(ref)
+    use32 = seed % 4 == 0 and int(o2.max()) < (1 << 32)
+    b = mi.PktBatch(buf, n, offs=dev_tensor(o2.astype(np.int64)),
+                    lens=dev_tensor(l2.astype(np.int32)), packed=layout != "slots", offs32=use32)
+    r = mi.ipv4_verify(b, bad_count=True)
+    assert np.array_equal(cpu(r["ip"]), ip_o), (seed, layout)
+    assert np.array_equal(cpu(r["l4"]), l4_o), (seed, layout)
+    assert np.array_equal(cpu(r["status"]), st_o), (seed, layout)
+    assert int(r["bad"].item()) == int((st_o != 0).sum()), (seed, layout)
+    if seed % 3 == 0:
+        out = dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"), l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
+                   status=torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda"))
+        torch.cuda.synchronize()
+        rep = mi.VerifyRepeat([b], [out], nstreams=1, engine="aql")
+        try:
+            rep.run(2)
+        finally:
+            rep.close()
+        assert np.array_equal(cpu(out["ip"]), ip_o), seed
+        assert np.array_equal(cpu(out["l4"]), l4_o), seed
+        assert np.array_equal(cpu(out["status"]), st_o), seed

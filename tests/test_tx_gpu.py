@@ -237,3 +237,38 @@ def test_tx_repeat_aql_needs_the_default_kernel(monkeypatch):
     want_dst, want_st = run_oracle(ORC, c)
     assert np.array_equal(st.cpu().numpy(), want_st)
     assert np.array_equal(tb.dst.cpu().numpy(), want_dst)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_tx_random_sweep(seed):
+    """Seeded random batches beyond the named edge cases: frame count, lengths
+    (20-9000 B), chain layout, protocol, IP header length, L3 offset and
+    destination alignment all drawn at random; the default TX kernel (and,
+    for every third seed, the AQL engine's entry point through the prepared
+    handle) byte for byte against the oracle, slots and status."""
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(1, 200))
+    hi = int(rng.choice([1500, 4000, 9000]))
+    lens = rng.integers(20, hi + 1, n)
+    layout = str(rng.choice(["socket", "single", "random"]))
+    proto = int(rng.choice([6, 17, 1]))
+    hl = rng.choice([20, 20, 20, 24, 40, 60], n)
+    l3 = int(rng.choice([0, 14, 18, 64]))
+    first = int(rng.integers(0, 256))
+    c = make_case(n, lens, layout=layout, seed=2000 + seed, proto=proto, hl=hl, l3=l3, dst_first=first,
+                  stride=9216 + 256)
+    want_dst, want_st = run_oracle(ORC, c)
+    got_dst, got_st = run_gpu(c)
+    assert np.array_equal(got_st, want_st), (seed, layout, np.nonzero(got_st != want_st)[0][:8])
+    bad = np.nonzero(got_dst != want_dst)[0]
+    assert bad.size == 0, (seed, layout, bad.size, bad[:8])
+    if seed % 3 == 0:
+        tb, st = _tx_batch(c)
+        torch.cuda.synchronize()
+        rep = mi.TxRepeat([tb], [st], nstreams=1, engine="aql")
+        try:
+            rep.run(2)
+        finally:
+            rep.close()
+        assert np.array_equal(st.cpu().numpy(), want_st), seed
+        assert np.array_equal(tb.dst.cpu().numpy(), want_dst), seed
