@@ -861,8 +861,8 @@ def test_verify_random_sweep(seed):
     random first offset, packed, shuffled, gappy), protocol and IP header
     length per packet, then random single-byte corruptions and truncated
     lengths.  ipv4_verify (and for every third seed the repeat handle's AQL
-    engine, for every fourth u32 offsets) against the oracle: ip / l4 /
-    status bit for bit."""
+    engine when the plan is one launch per pass, for every fourth u32
+    offsets) against the oracle: ip / l4 / status bit for bit."""
     rng = np.random.default_rng(5000 + seed)
     n = int(rng.integers(1, 3000))
     if rng.random() < 0.5:
@@ -905,7 +905,8 @@ def test_verify_random_sweep(seed):
     assert np.array_equal(cpu(r["l4"]), l4_o), (seed, layout)
     assert np.array_equal(cpu(r["status"]), st_o), (seed, layout)
     assert int(r["bad"].item()) == int((st_o != 0).sum()), (seed, layout)
-    if seed % 3 == 0:
+    # (length-class plans take several launches per pass: HIP engine only, -ENOTSUP by design)
+    if seed % 3 == 0 and "length classes" not in mi.verify_plan(b):
         out = dict(ip=torch.zeros(n, dtype=torch.uint16, device="cuda"), l4=torch.zeros(n, dtype=torch.uint16, device="cuda"),
                    status=torch.full((n,), 0xEE, dtype=torch.uint8, device="cuda"))
         torch.cuda.synchronize()
