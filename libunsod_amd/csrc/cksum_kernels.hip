@@ -358,10 +358,7 @@ __device__ __forceinline__ u32x4 ld16_keep(__amdgpu_buffer_rsrc_t r, uint32_t of
 // (LDS, 16 B per chunk of a pass) or, false, reloaded through L2 ahead of the
 // stream -- 2 KiB of LDS per wave instead of 10 (round 6: with a tighter
 // register budget, more waves per CU; entry points mi_aql_run<U>w2o).
-// D (round 6, experiment): datagrams per wave's range (64, or 32: twice the
-// waves, half the bytes each).
-template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false, bool PIPE = false, bool CAP = MI_RUN_CAPTURE,
-          uint32_t D = 64>
+template <int U, int MODE = 0, int NW = kBlock / 64, bool RG = false, bool PIPE = false, bool CAP = MI_RUN_CAPTURE>
 __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
                                             uint32_t *bad, const SpanSeeds &sp, uint32_t abs_lanes,
                                             const uint32_t *starts = nullptr, uint32_t nr = 0,
@@ -372,10 +369,9 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
   __shared__ u32x4 s_c[CAP ? NW : 1][CAP ? W : 1];  // the pass's chunks: header windows / last chunks come from here
   const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  static_assert(D == 64 || D == 32, "datagrams per range");
-  uint32_t rstride = gridDim.x * NW * D;
+  uint32_t rstride = gridDim.x * NW * 64u;
   uint32_t *sq = s_q[wv];
-  uint32_t p0 = (blockIdx.x * NW + wv) * D, cnt = D;
+  uint32_t p0 = (blockIdx.x * NW + wv) * 64u, cnt = 64u;
   if constexpr (RG) {
     const uint32_t w = blockIdx.x * NW + wv;
     if (w >= nr) return;
@@ -418,7 +414,7 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
     }
     const uint32_t pn = p0 + rstride;
     uint32_t offn = 0, flenn = 0;
-    if (pn + lane < d.n && lane < cnt) {
+    if (pn + lane < d.n) {
       offn = pkt_off(d, pn + lane);
       flenn = pkt_len(d, pn + lane);
     }
@@ -583,11 +579,11 @@ __device__ __forceinline__ void packed_body(const Desc &d, uint16_t *ip_out, uin
 #ifndef MI_RUN_MINW
 #define MI_RUN_MINW 1  // waves per SIMD the flat-run kernel is held to (register budget experiments)
 #endif
-template <int U, int MODE = 0, int NW = kBlock / 64, bool PIPE = false, uint32_t D = 64>
+template <int U, int MODE = 0, int NW = kBlock / 64, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_packed(Desc d, uint16_t *ip_out, uint16_t *l4_out,
                                                                 uint8_t *st_out, uint32_t *bad, SpanSeeds sp,
                                                                 uint32_t abs_lanes) {
-  packed_body<U, MODE, NW, false, PIPE, MI_RUN_CAPTURE, D>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
+  packed_body<U, MODE, NW, false, PIPE>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
 #ifndef MI_RUN_OCC_WAVES
 #define MI_RUN_OCC_WAVES 5
@@ -1471,11 +1467,6 @@ MI_AQL_RUN_W(8, 2)
   }
 MI_AQL_RUN_WP(4)
 MI_AQL_RUN_WP(8)
-// (the same with 32-datagram ranges: mi_aql_run8w2h)
-extern "C" __global__ __launch_bounds__(128) void mi_aql_run8w2h(Desc d, uint16_t *ip, uint16_t *l4, uint8_t *st,
-                                                                 uint32_t *bad) {
-  packed_body<8, 0, 2, false, false, MI_RUN_CAPTURE, 32>(d, ip, l4, st, bad, SpanSeeds{}, 0u);
-}
 // (the same, header windows reloaded instead of captured, held to
 // MI_RUN_OCC_WAVES waves per SIMD: mi_aql_run<U>w2o)
 #define MI_AQL_RUN_WO(U_, WV_)                                                                          \
@@ -2372,7 +2363,6 @@ struct Plan {
   int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
   bool pipe = false;  // kPlanRun, 2 waves: the pipelined passes (packed_body PIPE)
   bool occ = false;   // kPlanRun, 2 waves: header windows reloaded, 5 waves per SIMD (mi_aql_run<U>w2o)
-  int dpw = 64;       // kPlanRun: datagrams per wave's range (32: U = 8, 2 waves only; mi_aql_run8w2h)
 };
 
 // The LDS-DMA flat run (k_ipv4_verify_run_dma) for packed batches with offset
@@ -2435,18 +2425,6 @@ bool run_pipe() {
   }
   return v == 1;
 }
-// Datagrams per wave's range of the 2-wave U = 8 flat run (MI_CKSUM_RUN_DPW=32;
-// mi__set_run_dpw): 64 by default.
-std::atomic<int> g_run_dpw{0};
-int run_dpw() {
-  int v = g_run_dpw.load(std::memory_order_relaxed);
-  if (!v) {
-    const char *e = getenv("MI_CKSUM_RUN_DPW");
-    v = e && atoi(e) == 32 ? 32 : 64;
-    g_run_dpw.store(v, std::memory_order_relaxed);
-  }
-  return v;
-}
 // Waves per workgroup of the flat-run verify (MI_CKSUM_RUN_WAVES = 1, 2 or 4;
 // mi__set_run_waves for tests).  2 by default: on the 2^22 Pareto batch 2-wave
 // workgroups ran 196.8-197.5 us against 203.1-203.5 (4 waves) and 201.8-202.5
@@ -2482,7 +2460,6 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
     pl.run_nw = pl.run_u == 16 ? 4 : run_waves();
     pl.pipe = pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_pipe();
     pl.occ = !pl.pipe && pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_occ();
-    if (!pl.pipe && !pl.occ && pl.run_nw == 2 && pl.run_u == 8 && run_dpw() == 32) pl.dpw = 32;
     // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
     // offset / length arrays: batches whose arrays reach kOOB take the register
     // kernel, whose descriptor reads are 64-bit)
@@ -2495,15 +2472,15 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
 }
 
 // Grids of the flat-run and 64-byte-slot kernels: 64 datagrams per wave.
-unsigned run_blocks(const Desc &d, int nw = 4, int dpw = 64) {
+unsigned run_blocks(const Desc &d, int nw = 4) {
   static const int run_cap = [] {
     const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 16384;
   }();
   // (the cap counts 4-wave workgroups' worth of waves)
-  const int cap = (g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap) * (4 / nw) * (64 / dpw);
-  uint64_t blocks = ((uint64_t)d.n + (uint64_t)dpw * nw - 1) / ((uint64_t)dpw * nw);
+  const int cap = (g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap) * (4 / nw);
+  uint64_t blocks = ((uint64_t)d.n + 64u * nw - 1) / (64u * nw);
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
 }
@@ -2621,11 +2598,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
 #undef X
   }
   if (pl.kind == kPlanRun && pl.run_nw != 4) {
-    const dim3 grid(run_blocks(d, pl.run_nw, pl.dpw)), blk(64 * pl.run_nw);
-    if (pl.dpw == 32) {
-      VLAUNCH((k_ipv4_verify_packed<8, 0, 2, false, 32>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);
-      return launched();
-    }
+    const dim3 grid(run_blocks(d, pl.run_nw)), blk(64 * pl.run_nw);
 #define X(U_, NW_)                                                                                           \
   if (pl.run_u == U_ && pl.run_nw == NW_) {                                                                  \
     VLAUNCH((k_ipv4_verify_packed<U_, 0, NW_>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);         \
@@ -2902,7 +2875,7 @@ enum AqlKernelId {
   MI_DEAL_SHAPES(X)
 #undef X
   kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2, kAqlRun4w2p, kAqlRun8w2p,
-  kAqlRun4w2o, kAqlRun8w2o, kAqlRun8w2h,
+  kAqlRun4w2o, kAqlRun8w2o,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2916,7 +2889,7 @@ const char *const kAqlNames[kAqlKernels] = {
     MI_DEAL_SHAPES(X)
 #undef X
     "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
-    "mi_aql_run4w2p", "mi_aql_run8w2p", "mi_aql_run4w2o", "mi_aql_run8w2o", "mi_aql_run8w2h",
+    "mi_aql_run4w2p", "mi_aql_run8w2p", "mi_aql_run4w2o", "mi_aql_run8w2o",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -2931,7 +2904,7 @@ const void *const kAqlFuncs[kAqlKernels] = {
     (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
     (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
     (const void *)mi_aql_run4w2p, (const void *)mi_aql_run8w2p, (const void *)mi_aql_run4w2o,
-    (const void *)mi_aql_run8w2o, (const void *)mi_aql_run8w2h,
+    (const void *)mi_aql_run8w2o,
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3263,10 +3236,9 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks, b
     if (pl.run_nw == 1) *id = pl.run_u == 4 ? kAqlRun4w1 : kAqlRun8w1;
     else if (pl.run_nw == 2 && pl.occ) *id = pl.run_u == 4 ? kAqlRun4w2o : kAqlRun8w2o;
     else if (pl.run_nw == 2 && pl.pipe) *id = pl.run_u == 4 ? kAqlRun4w2p : kAqlRun8w2p;
-    else if (pl.run_nw == 2 && pl.dpw == 32) *id = kAqlRun8w2h;
     else if (pl.run_nw == 2) *id = pl.run_u == 4 ? kAqlRun4w2 : kAqlRun8w2;
     else *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
-    *blocks = run_blocks(d, pl.run_nw, pl.dpw);
+    *blocks = run_blocks(d, pl.run_nw);
     return 0;
   }
   if (pl.kind == kPlanSlot64) {
@@ -3391,7 +3363,6 @@ unsigned aql_wg(int id) {
   switch (id) {
     case kAqlRun4w1: case kAqlRun8w1: return 64;
     case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: case kAqlRun4w2o: case kAqlRun8w2o:
-    case kAqlRun8w2h:
       return 128;
     case kAqlScalar: return kScalarThreads;
     case kAqlTx: return 64;
@@ -4202,14 +4173,6 @@ int mi__set_run_pipe(int on) {
   g_run_pipe.store(on ? 1 : 0);
   return was;
 }
-// 32-datagram ranges for the 2-wave U = 8 flat run (32) or the default (64);
-// returns the previous setting.
-int mi__set_run_dpw(int dpw) {
-  const int was = run_dpw();
-  if (dpw != 32 && dpw != 64) return set_err(-EINVAL, "run datagrams per wave %d", dpw);
-  g_run_dpw.store(dpw);
-  return was;
-}
 int mi__set_run_waves(int w) {
   if (w != 1 && w != 2 && w != 4) return set_err(-EINVAL, "run waves %d", w);
   g_run_waves.store(w);
@@ -4442,7 +4405,6 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
              pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>"
              : pl.pipe      ? "k_ipv4_verify_packed<%d,%d waves,pipelined>"
              : pl.occ       ? "k_ipv4_verify_packed_occ<%d,%d waves>"
-             : pl.dpw == 32 ? "k_ipv4_verify_packed<%d,%d waves,32-datagram ranges>"
                             : "k_ipv4_verify_packed<%d,%d waves>",
              pl.run_u, pl.run_nw);
   else if (pl.kind == kPlanShape)

@@ -351,21 +351,19 @@ def test_packed_layout_golden(golden):
     assert int(r["bad"].item()) == int((g["ver_st"] != 0).sum())
 
 
-@pytest.mark.parametrize("variant", [(4, 0, 0, 64), (8, 1, 0, 64), (4, 1, 0, 64), (8, 0, 1, 64), (4, 0, 1, 64),
-                                     (8, 0, 0, 32)])
+@pytest.mark.parametrize("variant", [(4, 0, 0), (8, 1, 0), (4, 1, 0), (8, 0, 1), (4, 0, 1)])
 def test_packed_variants_golden(golden, variant):
     """The flat-run kernel's round-6 variants -- chunks per pass U, pipelined
     passes (mi__set_run_pipe), header windows reloaded at a tighter register
-    budget (mi__set_run_occ), 32-datagram ranges (mi__set_run_dpw) -- on the
-    golden RX batch (HIP launches) and on a Pareto batch through the AQL
-    engine, bit-exact."""
+    budget (mi__set_run_occ) -- on the golden RX batch (HIP launches) and on a
+    Pareto batch through the AQL engine, bit-exact."""
     import ctypes as C
     lib = mi.load()
-    for f in ("mi__set_packed_u", "mi__set_run_pipe", "mi__set_run_occ", "mi__set_run_dpw"):
+    for f in ("mi__set_packed_u", "mi__set_run_pipe", "mi__set_run_occ"):
         getattr(lib, f).restype = C.c_int
         getattr(lib, f).argtypes = [C.c_int]
-    u, pipe, occ, dpw = variant
-    was = (lib.mi__set_packed_u(u), lib.mi__set_run_pipe(pipe), lib.mi__set_run_occ(occ), lib.mi__set_run_dpw(dpw))
+    u, pipe, occ = variant
+    was = (lib.mi__set_packed_u(u), lib.mi__set_run_pipe(pipe), lib.mi__set_run_occ(occ))
     try:
         test_packed_layout_golden(golden)
         n = 20000
@@ -389,7 +387,6 @@ def test_packed_variants_golden(golden, variant):
         lib.mi__set_packed_u(was[0])
         lib.mi__set_run_pipe(was[1])
         lib.mi__set_run_occ(was[2])
-        lib.mi__set_run_dpw(was[3])
 
 
 @pytest.mark.parametrize("layout", ["packed", "shuffled", "gappy"])
