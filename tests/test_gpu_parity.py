@@ -918,3 +918,46 @@ def test_verify_random_sweep(seed):
         assert np.array_equal(cpu(out["ip"]), ip_o), seed
         assert np.array_equal(cpu(out["l4"]), l4_o), seed
         assert np.array_equal(cpu(out["status"]), st_o), seed
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_finalize_random_sweep(seed):
+    """TX finalize in place (in_delayed_cksum + ip_sum) on seeded random
+    batches: slots or packed / gappy offsets, lengths 20-9000 B, TCP / UDP /
+    ICMP / others, IP options, truncated available lengths, with and without
+    MI_BATCH_DEMUX (the small-header senders and fragments).  The whole
+    buffer after the GPU pass equals the oracle's, bytes between datagrams
+    included."""
+    rng = np.random.default_rng(7000 + seed)
+    n = int(rng.integers(1, 2000))
+    lens = np.maximum(rng.integers(20, int(rng.choice([200, 1500, 9000])) + 1, n), 20).astype(np.int64)
+    proto = rng.choice([6, 17, 6, 17, 1, 2, 112, 47], n)
+    hl = np.minimum(rng.choice([20, 20, 20, 24, 40, 60], n), lens & ~3)
+    demux = bool(seed % 2)
+    layout = str(rng.choice(["slots", "packed", "gappy"]))
+    if layout == "slots":
+        stride = int(lens.max()) + int(rng.integers(0, 200))
+        first = int(rng.integers(0, 100))
+        b0 = synth.build_ipv4_batch(n, lens, stride=stride, first_off=first, seed=seed, proto=proto, hl=hl)
+        offs = (first + np.arange(n, dtype=np.int64) * stride).astype(np.uint64)
+    else:
+        offs = synth.packed_offsets(lens, first_off=int(rng.integers(0, 64)))
+        if layout == "gappy":
+            offs = offs + np.cumsum(rng.integers(0, 300, n)).astype(np.uint64)
+        b0 = synth.build_ipv4_batch(n, lens, offs=offs.astype(np.int64), seed=seed, proto=proto, hl=hl)
+    frag = rng.random(n) < 0.05  # fragments: MF or an offset
+    for i in np.nonzero(frag)[0]:
+        b0["buf"][int(offs[i]) + 6] = int(rng.choice([0x20, 0x00, 0x21]))
+        b0["buf"][int(offs[i]) + 7] = int(rng.integers(1, 256))
+    flen = lens.astype(np.uint32).copy()
+    cut = rng.choice(n, int(rng.integers(0, max(1, n // 20) + 1)), replace=False)
+    flen[cut] = (flen[cut] * rng.random(cut.size)).astype(np.uint32)
+    _, want = aligned(b0["buf"])
+    ORC.ipv4_finalize_batch(want, n, offs=offs, flen=flen, demux=demux)
+    buf = dev_tensor(b0["buf"])
+    b = mi.PktBatch(buf, n, offs=dev_tensor(offs.astype(np.int64)), lens=dev_tensor(flen.astype(np.int32)),
+                    packed=layout == "packed", demux=demux)
+    mi.ipv4_finalize(b)
+    got = cpu(buf)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, (seed, layout, demux, bad.size, bad[:8])
