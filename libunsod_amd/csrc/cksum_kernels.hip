@@ -612,12 +612,8 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
   uint32_t *sq = s_q[wv];
   const bool demux = d.flags & MI_BATCH_DEMUX;
   // one datagram's outputs from its sums (the flat run's epilogue, MODE 0)
-  // (registers: the header window's third chunk is reloaded through L2 only
-  // when the IPv4 header reaches it, and the last chunk is kept as its partial
-  // sum -- 137 -> 4-wave budgets)
-  auto fin = [&](uint32_t i, uint32_t off, uint32_t flen, uint32_t h, uint32_t qs, uint32_t qe_t,
-                 const u32x4 &h0, const u32x4 &h1) {
-    const u32x4 h2 = h > 12u ? ld16_keep(r, (off & ~15u) + 32u) : u32x4{0, 0, 0, 0};
+  auto fin = [&](uint32_t i, uint32_t off, uint32_t flen, uint32_t h, uint32_t t, uint32_t qs, uint32_t qe,
+                 const u32x4 &h0, const u32x4 &h1, const u32x4 &h2, const u32x4 &tv) {
     const u32x4 hv[3] = {h0, h1, h2};
     const IpHdr ih = parse_ipv4<1, 3>(hv, h);
     const bool odd = h & 1u;
@@ -625,7 +621,7 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
     const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
     const uint32_t hend = hdr_ok ? ih.hl : 0u;
     const uint32_t lend = len_ok ? ih.iplen : hend;
-    uint32_t total = qe_t - (qs + range_sum(h0, 0, 0, (int)h));
+    uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(h0, 0, 0, (int)h));
     uint32_t hdr = 0;
     if (hend == 20u) {
       hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
@@ -633,7 +629,7 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
     } else if (hend > 20u) {
 #pragma unroll
       for (uint32_t k = 0; k < 5; ++k) {
-        const u32x4 x = k == 0 ? h0 : k == 1 ? h1 : ld16(r, (off & ~15u) + 16u * k);
+        const u32x4 x = k == 0 ? h0 : k == 1 ? h1 : k == 2 ? h2 : ld16(r, (off & ~15u) + 16u * k);
         hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
       }
     }
@@ -684,8 +680,8 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
     const uint32_t csA = stA >> 4, ceA = enA >> 4, hA = stA & 15u, tA = enA & 15u;
     const uint32_t csB = stB >> 4, ceB = enB >> 4, hB = stB & 15u, tB = enB & 15u;
     const u32x4 z{0, 0, 0, 0};
-    u32x4 a0 = z, a1 = z, b0 = z, b1 = z;
-    uint32_t carry = 0, qsA = 0, qeA = 0, qsB = 0, qeB = 0, ptA = 0, ptB = 0;  // pt: the last chunk's partial sum
+    u32x4 a0 = z, a1 = z, a2 = z, at = z, b0 = z, b1 = z, b2 = z, bt = z;
+    uint32_t carry = 0, qsA = 0, qeA = 0, qsB = 0, qeB = 0;
     for (uint32_t cb = 0;;) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -705,12 +701,14 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
       if (aA) {
         if (csA - cb < W) a0 = s_c[wv][csA - cb];
         if (csA + 1u - cb < W) a1 = s_c[wv][csA + 1u - cb];
-        if (tA && ceA - cb < W) ptA = range_sum(s_c[wv][ceA - cb], 0, 0, (int)tA);
+        if (csA + 2u - cb < W) a2 = s_c[wv][csA + 2u - cb];
+        if (tA && ceA - cb < W) at = s_c[wv][ceA - cb];
       }
       if (aB) {
         if (csB - cb < W) b0 = s_c[wv][csB - cb];
         if (csB + 1u - cb < W) b1 = s_c[wv][csB + 1u - cb];
-        if (tB && ceB - cb < W) ptB = range_sum(s_c[wv][ceB - cb], 0, 0, (int)tB);
+        if (csB + 2u - cb < W) b2 = s_c[wv][csB + 2u - cb];
+        if (tB && ceB - cb < W) bt = s_c[wv][ceB - cb];
       }
       cb += W;
       if (cb >= nch) break;
@@ -723,8 +721,8 @@ __device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, 
     }
     if (ceA >= nch) qeA = carry;
     if (ceB >= nch) qeB = carry;
-    if (aA) fin(iA, offA, flA, hA, qsA, qeA + ptA, a0, a1);
-    if (aB) fin(iB, offB, flB, hB, qsB, qeB + ptB, b0, b1);
+    if (aA) fin(iA, offA, flA, hA, tA, qsA, qeA, a0, a1, a2, at);
+    if (aB) fin(iB, offB, flB, hB, tB, qsB, qeB, b0, b1, b2, bt);
     __builtin_amdgcn_wave_barrier();
   }
 }
