@@ -594,143 +594,6 @@ __global__ __launch_bounds__(128, WV) void k_ipv4_verify_packed_occ(Desc d, uint
                                                                 uint32_t abs_lanes) {
   packed_body<U, 0, 2, false, false, false>(d, ip_out, l4_out, st_out, bad, sp, abs_lanes);
 }
-// Round 6 experiment (X2): 128-datagram ranges, two datagrams per lane (A =
-// p0 + lane, B = p0 + 64 + lane), one flat stream over the whole range, so a
-// wave's fixed start (descriptors, r0 / r1, the partly empty last pass) is paid
-// once per ~36 KB instead of ~18 KB (32-datagram ranges, half the bytes per
-// start, measured 16 % slower: profiles/r06/run_dpw_ab_r06.jsonl).  Verify
-// only; a grid of one range per wave (no grid-stride prefetch).
-template <int U, int NW>
-__device__ __forceinline__ void packed_body_x2(const Desc &d, uint16_t *ip_out, uint16_t *l4_out, uint8_t *st_out,
-                                               uint32_t *bad) {
-  constexpr uint32_t W = 64u * U;
-  __shared__ uint32_t s_q[NW][W];
-  __shared__ u32x4 s_c[NW][W];
-  const __amdgpu_buffer_rsrc_t r = rsrc_of(d);
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t rstride = gridDim.x * NW * 128u;
-  uint32_t *sq = s_q[wv];
-  const bool demux = d.flags & MI_BATCH_DEMUX;
-  // one datagram's outputs from its sums (the flat run's epilogue, MODE 0)
-  auto fin = [&](uint32_t i, uint32_t off, uint32_t flen, uint32_t h, uint32_t t, uint32_t qs, uint32_t qe,
-                 const u32x4 &h0, const u32x4 &h1, const u32x4 &h2, const u32x4 &tv) {
-    const u32x4 hv[3] = {h0, h1, h2};
-    const IpHdr ih = parse_ipv4<1, 3>(hv, h);
-    const bool odd = h & 1u;
-    const bool hdr_ok = flen >= 20u && ih.hl >= 20u && ih.hl <= flen;
-    const bool len_ok = hdr_ok && ih.iplen >= ih.hl && ih.iplen <= flen;
-    const uint32_t hend = hdr_ok ? ih.hl : 0u;
-    const uint32_t lend = len_ok ? ih.iplen : hend;
-    uint32_t total = (qe + range_sum(tv, 0, 0, (int)t)) - (qs + range_sum(h0, 0, 0, (int)h));
-    uint32_t hdr = 0;
-    if (hend == 20u) {
-      hdr = abs_halves(ih.w[0], odd) + abs_halves(ih.w[1], odd) + abs_halves(ih.w[2], odd) +
-            abs_halves(ih.w[3], odd) + abs_halves(ih.w[4], odd);
-    } else if (hend > 20u) {
-#pragma unroll
-      for (uint32_t k = 0; k < 5; ++k) {
-        const u32x4 x = k == 0 ? h0 : k == 1 ? h1 : k == 2 ? h2 : ld16(r, (off & ~15u) + 16u * k);
-        hdr += range_sum(x, (int)(16u * k) - (int)h, 0, (int)hend);
-      }
-    }
-    if (lend < flen)
-      for (uint32_t c = (off + lend) & ~15u; c < off + flen; c += 16u)
-        total -= range_sum(ld16(r, c), (int)(c - off), (int)lend, (int)flen);
-    verify_emit(verify_result(i, odd, ih, hdr_ok, len_ok, hdr, total - hdr, d, r, off), ip_out, l4_out, st_out, bad, d);
-  };
-  for (uint32_t p0 = (blockIdx.x * NW + wv) * 128u; p0 < d.n; p0 += rstride) {
-    const uint32_t iA = p0 + lane, iB = p0 + 64u + lane;
-    const bool aA = iA < d.n, aB = iB < d.n;
-    const uint32_t offA = aA ? pkt_off(d, iA) : 0u, flA = aA ? pkt_len(d, iA) : 0u;
-    const uint32_t offB = aB ? pkt_off(d, iB) : 0u, flB = aB ? pkt_len(d, iB) : 0u;
-    const uint32_t endA = aA ? offA + flA : 0u, endB = aB ? offB + flB : 0u;
-    const bool sane = (!aA || (offA < kOOB && endA >= offA && endA <= d.bytes)) &&
-                      (!aB || (offB < kOOB && endB >= offB && endB <= d.bytes));
-    const uint32_t r0 = wave_min(min(aA ? offA : ~0u, aB ? offB : ~0u)) & ~15u;
-    const uint32_t r1 = wave_max(max(endA, endB));
-    const uint32_t nch = (r1 - r0 + 15u) >> 4;
-    const uint32_t dbytes = wave_total((aA ? min(flA, 0xffffu) : 0u) + (aB ? min(flB, 0xffffu) : 0u));
-    const bool packed = __all(sane) && (uint64_t)nch * 16u <= 2ull * dbytes + 4096u;
-    if (!packed) {  // one lane per datagram, A then B
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const bool act = k ? aB : aA;
-        const uint32_t off = k ? offB : offA, flen = k ? flB : flA, i = k ? iB : iA;
-        if (act) {
-          u32x4 w[4];
-          issue_first<1, 4>(r, off, flen, 0, w);
-          IpHdr ih;
-          bool hdr_ok, l4_ok;
-          uint32_t sum_h, sum_l;
-          ipv4_sums<1, 4, false>(r, off, flen, 0, w, ih, hdr_ok, l4_ok, sum_h, sum_l, demux);
-          verify_emit(verify_result(i, ((uintptr_t)d.base + off) & 1u, ih, hdr_ok, l4_ok, sum_h, sum_l, d, r, off),
-                      ip_out, l4_out, st_out, bad, d);
-        }
-      }
-      continue;
-    }
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t c = 64u * u + lane;
-      v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
-    }
-    const uint32_t stA = aA ? offA - r0 : 0u, enA = aA ? endA - r0 : 0u;
-    const uint32_t stB = aB ? offB - r0 : 0u, enB = aB ? endB - r0 : 0u;
-    const uint32_t csA = stA >> 4, ceA = enA >> 4, hA = stA & 15u, tA = enA & 15u;
-    const uint32_t csB = stB >> 4, ceB = enB >> 4, hB = stB & 15u, tB = enB & 15u;
-    const u32x4 z{0, 0, 0, 0};
-    u32x4 a0 = z, a1 = z, a2 = z, at = z, b0 = z, b1 = z, b2 = z, bt = z;
-    uint32_t carry = 0, qsA = 0, qeA = 0, qsB = 0, qeB = 0;
-    for (uint32_t cb = 0;;) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t x = sum4(v[u]);  // chunks past the run load as zeros
-        const uint32_t inc = wave_scan(x);
-        sq[64u * u + lane] = carry + inc - x;
-        s_c[wv][64u * u + lane] = v[u];
-        carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (csA - cb < W) qsA = sq[csA - cb];
-      if (ceA - cb < W) qeA = sq[ceA - cb];
-      if (csB - cb < W) qsB = sq[csB - cb];
-      if (ceB - cb < W) qeB = sq[ceB - cb];
-      if (aA) {
-        if (csA - cb < W) a0 = s_c[wv][csA - cb];
-        if (csA + 1u - cb < W) a1 = s_c[wv][csA + 1u - cb];
-        if (csA + 2u - cb < W) a2 = s_c[wv][csA + 2u - cb];
-        if (tA && ceA - cb < W) at = s_c[wv][ceA - cb];
-      }
-      if (aB) {
-        if (csB - cb < W) b0 = s_c[wv][csB - cb];
-        if (csB + 1u - cb < W) b1 = s_c[wv][csB + 1u - cb];
-        if (csB + 2u - cb < W) b2 = s_c[wv][csB + 2u - cb];
-        if (tB && ceB - cb < W) bt = s_c[wv][ceB - cb];
-      }
-      cb += W;
-      if (cb >= nch) break;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t c = cb + 64u * u + lane;
-        v[u] = ld16(r, c < nch ? r0 + 16u * c : kOOB);
-      }
-      __builtin_amdgcn_wave_barrier();  // lookups done before the next pass rewrites s_q / s_c
-    }
-    if (ceA >= nch) qeA = carry;
-    if (ceB >= nch) qeB = carry;
-    if (aA) fin(iA, offA, flA, hA, tA, qsA, qeA, a0, a1, a2, at);
-    if (aB) fin(iB, offB, flB, hB, tB, qsB, qeB, b0, b1, b2, bt);
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-template <int U>
-__global__ __launch_bounds__(128, MI_RUN_MINW) void k_ipv4_verify_packed_x2(Desc d, uint16_t *ip_out, uint16_t *l4_out,
-                                                                        uint8_t *st_out, uint32_t *bad) {
-  packed_body_x2<U, 2>(d, ip_out, l4_out, st_out, bad);
-}
 template <int U, int NW>
 __global__ __launch_bounds__(64 * NW, MI_RUN_MINW) void k_ipv4_verify_ranges(Desc d, uint16_t *ip_out, uint16_t *l4_out,
                                                                 uint8_t *st_out, uint32_t *bad, const uint32_t *starts,
@@ -1604,11 +1467,6 @@ MI_AQL_RUN_W(8, 2)
   }
 MI_AQL_RUN_WP(4)
 MI_AQL_RUN_WP(8)
-// (128-datagram ranges, two datagrams per lane: mi_aql_run8w2x)
-extern "C" __global__ __launch_bounds__(128, MI_RUN_MINW) void mi_aql_run8w2x(Desc d, uint16_t *ip, uint16_t *l4,
-                                                                             uint8_t *st, uint32_t *bad) {
-  packed_body_x2<8, 2>(d, ip, l4, st, bad);
-}
 // (the same, header windows reloaded instead of captured, held to
 // MI_RUN_OCC_WAVES waves per SIMD: mi_aql_run<U>w2o)
 #define MI_AQL_RUN_WO(U_, WV_)                                                                          \
@@ -2505,7 +2363,6 @@ struct Plan {
   int dma = 0;  // kPlanRun: 10 U + R of the LDS-DMA kernel (k_ipv4_verify_run_dma<U, R>), 0: the register one
   bool pipe = false;  // kPlanRun, 2 waves: the pipelined passes (packed_body PIPE)
   bool occ = false;   // kPlanRun, 2 waves: header windows reloaded, 5 waves per SIMD (mi_aql_run<U>w2o)
-  bool x2 = false;    // kPlanRun, 2 waves, U = 8: 128-datagram ranges, two per lane (mi_aql_run8w2x)
 };
 
 // The LDS-DMA flat run (k_ipv4_verify_run_dma) for packed batches with offset
@@ -2568,18 +2425,6 @@ bool run_pipe() {
   }
   return v == 1;
 }
-// 128-datagram ranges, two datagrams per lane, for the 2-wave U = 8 flat run
-// (MI_CKSUM_RUN_X2=1; mi__set_run_x2).
-std::atomic<int> g_run_x2{-1};
-bool run_x2() {
-  int v = g_run_x2.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char *e = getenv("MI_CKSUM_RUN_X2");
-    v = e && e[0] == '1' ? 1 : 0;
-    g_run_x2.store(v, std::memory_order_relaxed);
-  }
-  return v == 1;
-}
 // Waves per workgroup of the flat-run verify (MI_CKSUM_RUN_WAVES = 1, 2 or 4;
 // mi__set_run_waves for tests).  2 by default: on the 2^22 Pareto batch 2-wave
 // workgroups ran 196.8-197.5 us against 203.1-203.5 (4 waves) and 201.8-202.5
@@ -2615,7 +2460,6 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
     pl.run_nw = pl.run_u == 16 ? 4 : run_waves();
     pl.pipe = pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_pipe();
     pl.occ = !pl.pipe && pl.run_nw == 2 && (pl.run_u == 4 || pl.run_u == 8) && run_occ();
-    pl.x2 = !pl.pipe && !pl.occ && pl.run_nw == 2 && pl.run_u == 8 && run_x2();
     // (the DMA kernel's descriptor offsets are 32-bit byte offsets into the
     // offset / length arrays: batches whose arrays reach kOOB take the register
     // kernel, whose descriptor reads are 64-bit)
@@ -2628,15 +2472,15 @@ Plan verify_plan(const Desc &d, uint32_t max_len) {
 }
 
 // Grids of the flat-run and 64-byte-slot kernels: 64 datagrams per wave.
-unsigned run_blocks(const Desc &d, int nw = 4, int dpw = 64) {
+unsigned run_blocks(const Desc &d, int nw = 4) {
   static const int run_cap = [] {
     const char *e = getenv("MI_CKSUM_RUN_BLOCKS");
     const int v = e ? atoi(e) : 0;
     return v > 0 ? v : 16384;
   }();
   // (the cap counts 4-wave workgroups' worth of waves)
-  const int cap = (g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap) * (4 / nw) * 64 / dpw;
-  uint64_t blocks = ((uint64_t)d.n + (uint64_t)dpw * nw - 1) / ((uint64_t)dpw * nw);
+  const int cap = (g_tune.max_blocks > 0 ? g_tune.max_blocks : run_cap) * (4 / nw);
+  uint64_t blocks = ((uint64_t)d.n + 64u * nw - 1) / (64u * nw);
   if (blocks > (uint64_t)cap) blocks = cap;
   return blocks ? (unsigned)blocks : 1u;
 }
@@ -2754,11 +2598,7 @@ int launch_verify(const Desc &d, uint32_t max_len, uint16_t *ip, uint16_t *l4, u
 #undef X
   }
   if (pl.kind == kPlanRun && pl.run_nw != 4) {
-    const dim3 grid(run_blocks(d, pl.run_nw, pl.x2 ? 128 : 64)), blk(64 * pl.run_nw);
-    if (pl.x2) {
-      VLAUNCH((k_ipv4_verify_packed_x2<8>), grid, blk, 0, s, d, ip, l4, st, bad);
-      return launched();
-    }
+    const dim3 grid(run_blocks(d, pl.run_nw)), blk(64 * pl.run_nw);
 #define X(U_, NW_)                                                                                           \
   if (pl.run_u == U_ && pl.run_nw == NW_) {                                                                  \
     VLAUNCH((k_ipv4_verify_packed<U_, 0, NW_>), grid, blk, 0, s, d, ip, l4, st, bad, SpanSeeds{}, 0u);         \
@@ -3035,7 +2875,7 @@ enum AqlKernelId {
   MI_DEAL_SHAPES(X)
 #undef X
   kAqlRun4, kAqlRun8, kAqlRun16, kAqlRun4w1, kAqlRun4w2, kAqlRun8w1, kAqlRun8w2, kAqlRun4w2p, kAqlRun8w2p,
-  kAqlRun4w2o, kAqlRun8w2o, kAqlRun8w2x,
+  kAqlRun4w2o, kAqlRun8w2o,
 #define X(U_, R_) kAqlRunDma_##U_##x##R_,
   MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3049,7 +2889,7 @@ const char *const kAqlNames[kAqlKernels] = {
     MI_DEAL_SHAPES(X)
 #undef X
     "mi_aql_run4", "mi_aql_run8", "mi_aql_run16", "mi_aql_run4w1", "mi_aql_run4w2", "mi_aql_run8w1", "mi_aql_run8w2",
-    "mi_aql_run4w2p", "mi_aql_run8w2p", "mi_aql_run4w2o", "mi_aql_run8w2o", "mi_aql_run8w2x",
+    "mi_aql_run4w2p", "mi_aql_run8w2p", "mi_aql_run4w2o", "mi_aql_run8w2o",
 #define X(U_, R_) "mi_aql_rundma_" #U_ "x" #R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3064,7 +2904,7 @@ const void *const kAqlFuncs[kAqlKernels] = {
     (const void *)mi_aql_run4, (const void *)mi_aql_run8, (const void *)mi_aql_run16, (const void *)mi_aql_run4w1,
     (const void *)mi_aql_run4w2, (const void *)mi_aql_run8w1, (const void *)mi_aql_run8w2,
     (const void *)mi_aql_run4w2p, (const void *)mi_aql_run8w2p, (const void *)mi_aql_run4w2o,
-    (const void *)mi_aql_run8w2o, (const void *)mi_aql_run8w2x,
+    (const void *)mi_aql_run8w2o,
 #define X(U_, R_) (const void *)mi_aql_rundma_##U_##x##R_,
     MI_RUN_DMA_SHAPES(X)
 #undef X
@@ -3396,10 +3236,9 @@ int aql_kernel_for(const Desc &d, uint32_t max_len, int *id, unsigned *blocks, b
     if (pl.run_nw == 1) *id = pl.run_u == 4 ? kAqlRun4w1 : kAqlRun8w1;
     else if (pl.run_nw == 2 && pl.occ) *id = pl.run_u == 4 ? kAqlRun4w2o : kAqlRun8w2o;
     else if (pl.run_nw == 2 && pl.pipe) *id = pl.run_u == 4 ? kAqlRun4w2p : kAqlRun8w2p;
-    else if (pl.run_nw == 2 && pl.x2) *id = kAqlRun8w2x;
     else if (pl.run_nw == 2) *id = pl.run_u == 4 ? kAqlRun4w2 : kAqlRun8w2;
     else *id = pl.run_u == 4 ? kAqlRun4 : pl.run_u == 16 ? kAqlRun16 : kAqlRun8;
-    *blocks = run_blocks(d, pl.run_nw, pl.x2 ? 128 : 64);
+    *blocks = run_blocks(d, pl.run_nw);
     return 0;
   }
   if (pl.kind == kPlanSlot64) {
@@ -3524,7 +3363,6 @@ unsigned aql_wg(int id) {
   switch (id) {
     case kAqlRun4w1: case kAqlRun8w1: return 64;
     case kAqlRun4w2: case kAqlRun8w2: case kAqlRun4w2p: case kAqlRun8w2p: case kAqlRun4w2o: case kAqlRun8w2o:
-    case kAqlRun8w2x:
       return 128;
     case kAqlScalar: return kScalarThreads;
     case kAqlTx: return 64;
@@ -4335,12 +4173,6 @@ int mi__set_run_pipe(int on) {
   g_run_pipe.store(on ? 1 : 0);
   return was;
 }
-// 128-datagram ranges (two datagrams per lane) on (1) / off (0); returns the previous setting.
-int mi__set_run_x2(int on) {
-  const int was = run_x2() ? 1 : 0;
-  g_run_x2.store(on ? 1 : 0);
-  return was;
-}
 int mi__set_run_waves(int w) {
   if (w != 1 && w != 2 && w != 4) return set_err(-EINVAL, "run waves %d", w);
   g_run_waves.store(w);
@@ -4573,7 +4405,6 @@ const char *mi_cksum_verify_plan(const mi_pkt_batch *b) {
              pl.run_nw == 4 ? "k_ipv4_verify_packed<%d>"
              : pl.pipe      ? "k_ipv4_verify_packed<%d,%d waves,pipelined>"
              : pl.occ       ? "k_ipv4_verify_packed_occ<%d,%d waves>"
-             : pl.x2        ? "k_ipv4_verify_packed_x2<%d,%d waves,128-datagram ranges>"
                             : "k_ipv4_verify_packed<%d,%d waves>",
              pl.run_u, pl.run_nw);
   else if (pl.kind == kPlanShape)

@@ -351,8 +351,7 @@ def test_packed_layout_golden(golden):
     assert int(r["bad"].item()) == int((g["ver_st"] != 0).sum())
 
 
-@pytest.mark.parametrize("variant", [(4, 0, 0, 0), (8, 1, 0, 0), (4, 1, 0, 0), (8, 0, 1, 0), (4, 0, 1, 0),
-                                     (8, 0, 0, 1)])
+@pytest.mark.parametrize("variant", [(4, 0, 0), (8, 1, 0), (4, 1, 0), (8, 0, 1), (4, 0, 1)])
 def test_packed_variants_golden(golden, variant):
     """The flat-run kernel's round-6 variants -- chunks per pass U, pipelined
     passes (mi__set_run_pipe), header windows reloaded at a tighter register
@@ -360,11 +359,11 @@ def test_packed_variants_golden(golden, variant):
     Pareto batch through the AQL engine, bit-exact."""
     import ctypes as C
     lib = mi.load()
-    for f in ("mi__set_packed_u", "mi__set_run_pipe", "mi__set_run_occ", "mi__set_run_x2"):
+    for f in ("mi__set_packed_u", "mi__set_run_pipe", "mi__set_run_occ"):
         getattr(lib, f).restype = C.c_int
         getattr(lib, f).argtypes = [C.c_int]
-    u, pipe, occ, x2 = variant
-    was = (lib.mi__set_packed_u(u), lib.mi__set_run_pipe(pipe), lib.mi__set_run_occ(occ), lib.mi__set_run_x2(x2))
+    u, pipe, occ = variant
+    was = (lib.mi__set_packed_u(u), lib.mi__set_run_pipe(pipe), lib.mi__set_run_occ(occ))
     try:
         test_packed_layout_golden(golden)
         n = 20000
@@ -388,7 +387,6 @@ def test_packed_variants_golden(golden, variant):
         lib.mi__set_packed_u(was[0])
         lib.mi__set_run_pipe(was[1])
         lib.mi__set_run_occ(was[2])
-        lib.mi__set_run_x2(was[3])
 
 
 @pytest.mark.parametrize("layout", ["packed", "shuffled", "gappy"])

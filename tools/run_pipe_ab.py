@@ -27,8 +27,6 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--waves", type=int, default=2)
-    ap.add_argument("--cases", default="0,0,0,0;4,0,1,0;0,0,1,0;4,0,0,0",
-                    help="';'-separated packed_u,pipe,occ,x2 cases (packed_u 0 = automatic)")
     args = ap.parse_args()
     import bench
     import libunsod_amd as mi
@@ -41,8 +39,6 @@ def main():
     lib.mi__set_packed_u.argtypes = [C.c_int]
     lib.mi__set_run_occ.restype = C.c_int
     lib.mi__set_run_occ.argtypes = [C.c_int]
-    lib.mi__set_run_x2.restype = C.c_int
-    lib.mi__set_run_x2.argtypes = [C.c_int]
     lib.mi__set_run_waves(args.waves)
     mi.set_busy_wait(True)
     dev = torch.device("cuda", 0)
@@ -51,12 +47,10 @@ def main():
         L_sum, n = wl["L_sum"], wl["n"]
         alg = L_sum + 5 * n
         for rnd in range(args.rounds):
-            for case in args.cases.split(";"):
-                pu, pipe, occ, x2 = (int(x) for x in case.split(","))
+            for pu, pipe, occ in ((0, 0, 0), (4, 0, 1), (0, 0, 1), (4, 0, 0)):
                 lib.mi__set_run_pipe(pipe)
                 lib.mi__set_packed_u(pu)
                 lib.mi__set_run_occ(occ)
-                lib.mi__set_run_x2(x2)
                 plan = bench.repeat_plan(wl["batches"][0])
                 rep = mi.VerifyRepeat(wl["batches"], wl["outs"], nstreams=2, engine="aql")
                 rep.run(200, timed=True)
@@ -71,13 +65,12 @@ def main():
                 rep.close()
                 chk = bench.check_timed_outputs(wl["outs"], args.steps)
                 us = span / args.steps
-                print(json.dumps(dict(config=cfg, round=rnd, pipe=pipe, occ=occ, x2=x2, packed_u=pu or "auto", plan=plan, us_per_launch=round(us, 2),
+                print(json.dumps(dict(config=cfg, round=rnd, pipe=pipe, occ=occ, packed_u=pu or "auto", plan=plan, us_per_launch=round(us, 2),
                                       frac=round(alg / us / 1e3 / bench.HBM_PEAK_GBS, 4),
                                       outputs_checked=chk["checked"])), flush=True)
         lib.mi__set_run_pipe(0)
         lib.mi__set_packed_u(0)
         lib.mi__set_run_occ(0)
-        lib.mi__set_run_x2(0)
         del wl
         torch.cuda.empty_cache()
 
