@@ -2782,7 +2782,7 @@ bool tx_default_lds() {
   const char *e = getenv("MI_CKSUM_TX_LDS");
   int u = 2, r = MI_TX_LDS_R;
   if (e && sscanf(e, "%dx%d", &u, &r) < 1) return false;
-  return u == 2 && r == MI_TX_LDS_R && !(e && (strchr(e, 'c') || strchr(e, 'g') || strchr(e, 'w')));
+  return u == 2 && r == MI_TX_LDS_R && !(e && (strchr(e, 'c') || strchr(e, 'g')));
 }
 bool tx_early_loads() {
   const char *e = getenv("MI_CKSUM_TX_EARLY");
@@ -2812,12 +2812,6 @@ int launch_tx(const TxDesc &t, Shape sh, hipStream_t s) {
     // call: A/B in one process); default 2 x MI_TX_LDS_R
     int u = 2, r = MI_TX_LDS_R;
     if (const char *e = getenv("MI_CKSUM_TX_LDS")) (void)sscanf(e, "%dx%d", &u, &r);
-    // two waves per workgroup, each with its own ring: "2x2w2"
-    if (const char *e = getenv("MI_CKSUM_TX_LDS"); e && u == 2 && r == 2 && strstr(e, "w2")) {
-      const unsigned g1 = tx_lds_grid(t.n, (unsigned)grid_for(t.n, 8));
-      hipLaunchKernelGGL((k_tx_lds<2, 2, tx_lds_waves(2, 2), false, 8, 2>), dim3((g1 + 1u) / 2u), dim3(128), 0, s, t);
-      return launched();
-    }
     // 16 lanes per frame (4 frames per wave, twice the waves): "2x2g16"
     if (const char *e = getenv("MI_CKSUM_TX_LDS"); e && u == 2 && r == 2 && strstr(e, "g16")) {
       hipLaunchKernelGGL((k_tx_lds<2, 2, tx_lds_waves(2, 2), false, 16>), dim3(tx_lds_grid(t.n, (unsigned)grid_for(t.n, 8), 16)),

@@ -1076,18 +1076,14 @@ __device__ __forceinline__ TxCut cut_unpack(uint32_t k, int q0) {
   return c;
 }
 // (the body, shared by k_tx_lds and the AQL engine's mi_aql_tx_lds)
-// NW: waves per workgroup (each with its own ring and frames; 1 by default).
-template <int U, int R, bool CC, int G = 8, int NW = 1>
+template <int U, int R, bool CC, int G = 8>
 __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
   static_assert(G == 8 || G == 16, "8 or 16 lanes per frame (4: 0.38 of 8 TB/s, profiles/r06/tx_g4_ab_r06.jsonl)");
-  constexpr uint32_t NG = 64 / G * NW;  // frames (lane groups) per workgroup
+  constexpr uint32_t NG = 64 / G;  // frames (lane groups) per wave = per workgroup
   static_assert(R >= 2 && R <= 4, "ring depth");
   __shared__ uint32_t s_seg[NG][kTxSeg][2];
-  __shared__ u32x4 s_ring_all[NW][R][2 * U][64];  // per wave, pass slot q % R: chunk u's A1 loads, then its A2 loads
-  __shared__ uint32_t s_cut_all[NW][CC ? R : 1][CC ? U : 1][64];  // CC: pass slot q % R's packed cuts
-  const uint32_t wv = NW > 1 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0u;
-  auto &s_ring = s_ring_all[wv];
-  auto &s_cut = s_cut_all[wv];
+  __shared__ u32x4 s_ring[R][2 * U][64];  // pass slot q % R: chunk u's A1 loads, then its A2 loads
+  __shared__ uint32_t s_cut[CC ? R : 1][CC ? U : 1][64];  // CC: pass slot q % R's packed cuts
   typedef __attribute__((address_space(3))) void *lds_ptr;
   Desc ds{}, dd{};
   ds.base = t.src;
@@ -1299,9 +1295,9 @@ __device__ __forceinline__ void tx_lds_body(const TxDesc &t) {
     if (!done) tx_frame_generic<G, U>(t, rs, rd, i, lane, len, k0, k1, ip_mlen);
   }
 }
-template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false, int G = 8, int NW = 1>
-__global__ __launch_bounds__(64 * NW, WV) void k_tx_lds(TxDesc t) {
-  tx_lds_body<U, R, CC, G, NW>(t);
+template <int U, int R, int WV = tx_lds_waves(U, R), bool CC = false, int G = 8>
+__global__ __launch_bounds__(64, WV) void k_tx_lds(TxDesc t) {
+  tx_lds_body<U, R, CC, G>(t);
 }
 // Its grid: one wave (64 / G frames) per workgroup; for G = 8 the same total
 // waves as k_tx_copy's 8 x 2 grid at the default cap (one frame group per

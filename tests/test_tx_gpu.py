@@ -117,7 +117,7 @@ def test_tx_copy_host_matches_oracle(mode):
         assert np.array_equal(dst[c["dst"].size:], np.zeros(dst.size - c["dst"].size, np.uint8)), name
 
 
-@pytest.mark.parametrize("kernel", ["wave", "pair", "lds", "lds1x3", "lds2x2c", "lds2x2g16", "lds2x2w2"])
+@pytest.mark.parametrize("kernel", ["wave", "pair", "lds", "lds1x3", "lds2x2c", "lds2x2g16"])
 def test_tx_kernel_every_case(kernel, monkeypatch):
     """The wave-per-frame TX kernel (k_tx_wave, MI_CKSUM_TX_KERNEL=wave), the
     lane-group gather through VGPRs (k_tx_copy, =pair) and through an LDS ring
@@ -126,7 +126,7 @@ def test_tx_kernel_every_case(kernel, monkeypatch):
     headers, short / nobufs / malformed frames, flags and data, UDP 0 ->
     0xffff), byte for byte against the oracle."""
     monkeypatch.setenv("MI_CKSUM_TX_KERNEL", kernel[:3] if kernel.startswith("lds") else kernel)
-    if kernel in ("lds1x3", "lds2x2c", "lds2x2g16", "lds2x2w2"):
+    if kernel in ("lds1x3", "lds2x2c", "lds2x2g16"):
         monkeypatch.setenv("MI_CKSUM_TX_LDS", kernel[3:])
     for name, c in CASES:
         want_dst, want_st = run_oracle(ORC, c)

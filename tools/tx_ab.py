@@ -32,7 +32,6 @@ VARIANTS = {
     "lds1x3": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="1x3"),  # 5 waves per SIMD
     "lds2x2c": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2c"),  # cut cache
     "lds2x2g16": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2g16"),  # 16 lanes per frame
-    "lds2x2w2": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2w2"),  # 2 waves per workgroup
     # the 2x2 ring with a smaller grid (mi_cksum_set_shape(0, 0, cap): cap
     # 4-wave workgroups' worth, i.e. 4 cap one-wave workgroups; 2048 = default)
     "lds2x2c1024": dict(MI_CKSUM_TX_KERNEL="lds", MI_CKSUM_TX_LDS="2x2", _cap=1024),
